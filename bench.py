@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""bench.py -- radar frames/s of the MI355X FMCW hot path (BASELINE.json metric).
+
+One step = one pass of the hot path (window -> range FFT -> corner turn -> Doppler FFT ->
+|X| map -> OS-CFAR -> ordered detection list) over one batch of synthetic frames already
+resident in HBM.  Workload at N=1: BASELINE config 2 -- 256 chirps x 1024 samples, fp32
+complex, 1 Rx, 1-D OS-CFAR 16 ref / 4 guard -- in batches of 1024 frames per GPU per step
+(= config 4's per-GPU share of 8192 frames at 8 GPUs; weak scaling).  With N > 1 each rank
+processes its own 1024 frames (frame sharding, no data-path collective) and the detection
+lists are gathered over RCCL inside the step (config 4).
+
+Launch: `python bench.py [--gpus N --steps K --warmup W]`, or for N > 1
+`python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
+ --master-port P bench.py --gpus N ...`.  Rank 0 prints ONE JSON line.
+
+roofline: the dominant kernel's algorithmic bytes per launch / its average launch duration,
+from HIP events the library records on the launch stream (fmcw_set_profiling) over a
+profiled repeat of the timed steps; traffic from profiles/pmc_<round>.json (rocprofv3
+FETCH_SIZE / WRITE_SIZE passes, gfx950 FETCH x2 correction) when present, else null.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "fpga-fmcw-radar-processor_amd"))
+
+HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+WORKLOADS = {
+    "c2": dict(ns=1024, nc=256, nrx=1, dtype="f32", cfar="os1d", frames=1024, recipe="two_targets",
+               desc="BASELINE config 2: 256 chirps x 1024 samples fp32, 1 Rx, OS-CFAR 1-D 16 ref / 4 guard"),
+    "c3": dict(ns=4096, nc=512, nrx=4, dtype="f32", cfar="os2d", frames=16, recipe="two_targets",
+               desc="BASELINE config 3: 512 chirps x 4096 samples fp32, 4 Rx NCI, 2-D OS-CFAR"),
+    "c5": dict(ns=8192, nc=1024, nrx=1, dtype="f16", cfar="os2d", frames=16, recipe="two_targets",
+               desc="BASELINE config 5: 1024 chirps x 8192 range bins, fp16 complex samples, 2-D OS-CFAR"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--frames", type=int, default=0, help="frames per GPU per step (0 = workload default)")
+    ap.add_argument("--chunk", type=int, default=0, help="frames per kernel chunk (0 = library auto)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-gather", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from fmcw import RadarCore, synth
+    from fmcw.dist import gather_detections
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    wl = dict(WORKLOADS[args.workload])
+    if args.frames:
+        wl["frames"] = args.frames
+    F, ns, nc, nrx = wl["frames"], wl["ns"], wl["nc"], wl["nrx"]
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    core = RadarCore(N_RANGE=ns, N_DOPPLER=nc, N_RX=nrx, in_dtype=wl["dtype"], cfar=wl["cfar"],
+                     max_frames=F, chunk_frames=args.chunk, device=local)
+    # synthetic input: 16 distinct frames (seed 1234 + global frame), tiled to F, resident in HBM
+    n_u = min(16, F)
+    first_global = rank * F
+    u = synth.frames(n_u, ns, nc, nrx, wl["recipe"], seed=1234 + first_global, dtype=wl["dtype"])
+    if wl["dtype"] == "f32":
+        u = u.view(np.float32)
+    ut = torch.from_numpy(np.ascontiguousarray(u)).to(dev)
+    reps = (F + n_u - 1) // n_u
+    cube = ut.repeat((reps,) + (1,) * (ut.dim() - 1))[:F].contiguous()
+    del ut
+    rd_map = torch.empty((F, ns, nc), dtype=torch.float32, device=dev)
+    det_cap = F * 4096
+    dets = torch.empty((det_cap, 4), dtype=torch.int32, device=dev)
+    n_dets = torch.zeros(4, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    gather = world > 1 and not args.no_gather
+    last = {}
+
+    def step():
+        core.enqueue(cube.data_ptr(), F, rd_map.data_ptr(), dets.data_ptr(), det_cap, n_dets.data_ptr(), stream)
+        if gather:
+            allr, counts = gather_detections(dets, n_dets[0], first_global)
+            last["total"] = int(allr.shape[0])
+
+    def timed(k):
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return float(el.item())
+
+    for _ in range(args.warmup):
+        step()
+    elapsed = timed(args.steps)
+    n_det_step = int(n_dets[0].item())
+
+    # profiled repeat: per-kernel durations from HIP events on the launch stream
+    core.reset_kernel_times()
+    core.set_profiling(True)
+    elapsed_prof = timed(args.steps)
+    kt = core.kernel_times()
+    core.set_profiling(False)
+
+    frames_total = world * F * args.steps
+    value = frames_total / elapsed
+    b_in = 8 if wl["dtype"] == "f32" else 4
+    px = ns * nc * nrx
+    ms_r, n_r = kt["k_range"]
+    ms_d, n_d = kt["k_doppler"]
+    bytes_range = F * args.steps * px * (b_in + 8)                 # stage A: cube in + spectrum out
+    bytes_dopp = F * args.steps * (px * 8 + ns * nc * 4)           # spectrum in + map out
+    kern = {}
+    for name, (ms, n) in kt.items():
+        if n:
+            kern[name] = {"launches_per_step": n // args.steps, "avg_ms": ms / n}
+    if ms_r:
+        kern["k_range"]["GBps_algorithmic"] = bytes_range / (ms_r * 1e-3) / 1e9
+    if ms_d:
+        kern["k_doppler"]["GBps_algorithmic"] = bytes_dopp / (ms_d * 1e-3) / 1e9
+    achieved = bytes_range / (ms_r * 1e-3) / 1e9 if ms_r else None
+    traffic = None
+    pmc_file = REPO / "profiles" / "pmc_r01.json"
+    if pmc_file.exists():
+        try:
+            pmc = json.loads(pmc_file.read_text())
+            if pmc.get("workload") == args.workload and pmc.get("frames_per_launch") == F // max(1, n_r // args.steps):
+                traffic = pmc.get("k_range_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"kernel": "k_range (window + range FFT + corner turn)", "bound": "hbm",
+                "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None, "traffic": traffic,
+                "bytes_per_launch": bytes_range // max(1, n_r),
+                "avg_launch_ms": round(ms_r / n_r, 5) if n_r else None}
+    e2e_bytes = F * (px * b_in + ns * nc * 4) + 16 * n_det_step
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, str(REPO / "oracle"))
+        import cpu_baseline as cb
+        uu = synth.frames(8, ns, nc, 1, wl["recipe"], seed=1234, dtype="f32")[:, 0]
+        m = cb.measure(ns, nc, lambda b: uu[:b], target_s=args.cpu_seconds, batch=8)
+        cpu = {"value": round(m["frames_per_s"], 2), "unit": "frames/s", "cores": m["workers"],
+               "kind": "port",
+               "sample": f"{m['frames']} frames of {ns}x{nc} (1 rx) fp32, NumPy/SciPy fp32 port of the oracle "
+                         f"(oracle/cpu_baseline.py), scipy.fft workers={m['workers']}, {m['seconds']:.1f} s"}
+
+    out = {
+        "metric": "radar frames/sec (range-Doppler+CFAR)",
+        "value": round(value, 1),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": wl["dtype"],
+        "data": "synthetic (tb_radar_core-style point targets + uniform noise, int16-quantised)",
+        "config": {"workload": wl["desc"], "frames_per_gpu_step": F, "n_chirps": nc,
+                   "n_samples": ns, "n_rx": nrx, "cfar": wl["cfar"], "rd_map": "linear fp32, written",
+                   "detection_gather": "rccl all_gather" if gather else "none (single GPU)",
+                   "parallelism": f"frame-sharded x{world}"},
+        "e2e_GBps_algorithmic": round(e2e_bytes * args.steps * world / elapsed / 1e9, 1),
+        "detections_per_step": n_det_step,
+        "roofline": roofline,
+        "kernels": kern,
+        "profiled_step_ms": round(elapsed_prof / args.steps * 1e3, 4),
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    core.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

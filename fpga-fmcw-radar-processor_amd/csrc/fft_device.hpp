@@ -1,0 +1,246 @@
+// fft_device.hpp -- LDS-staged Stockham FFT building blocks for gfx950 (CDNA4, wave64).
+//
+// Replaces the Xilinx LogiCORE FFT v9.1 instances of the reference
+// (rtl/src/radar_core.vhd:303-316 range FFT, :351-364 Doppler FFT; forward transform,
+// config word x"0001" at :247; natural-order output, xfft_0.xci:12-27).  The build spec is
+// an *unscaled* fp32 forward DFT X[k] = sum_n x[n] exp(-2 pi i k n / N):
+// the IP's block-floating-point exponent is discarded by the reference (:310) and is not
+// reproduced.
+//
+// Decomposition (N = 2^n, 64 <= N <= 8192): P = N/16 threads per transform, 16 complex
+// values per thread.  Pass 0 is radix-8 over stride N/8 taken straight from registers, so a
+// thread's first-pass inputs are the 16-byte pairs (2t, 2t+1) + (N/8) m -- i.e. 16 B/lane
+// coalesced loads.  Further passes are radix-16 while >= 16 points remain, then one final
+// radix-2/4/8 pass, each a Stockham autosort step through LDS:
+//     group j, k = j mod L:  v[m] = x[j + m N/R] * w_{LR}^{m k};  V = DFT_R(v);
+//     y[(j/L) L R + k + m L] = V[m]
+// LDS rows are padded by one complex per 16 (index i -> i + i/16) against bank conflicts.
+// Twiddles: w^1, w^2, w^4, w^8 from v_sin_f32 / v_cos_f32 (argument in revolutions, exact
+// k/LR fractions), other powers as products (GroupTwiddles).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fmcw {
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 mul_negi(float2 a) { return make_float2(a.y, -a.x); }  // -i a
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+
+constexpr int padded(int n) { return n + n / 16; }
+__device__ __forceinline__ int pad16(int i) { return i + (i >> 4); }
+// pad16(x + o) for a compile-time offset o = m*S (S a power of two) when x % 16 < S or
+// S % 16 == 0 -- true for every Stockham read (x = j < N/R) and write (x % 16 = k < L):
+// the padded address is then pad16(x) plus an immediate, so ds_read/ds_write use offsets.
+constexpr int padoff(int o) { return o + o / 16; }
+
+// Loop-invariant values (lane index, twiddles, LDS addresses) would otherwise be hoisted out of
+// the grid-stride loops by LICM and pinned in ~150 VGPRs; an opaque copy per iteration keeps
+// them as cheap recomputation instead (occupancy matters more here than a few VALU ops).
+__device__ __forceinline__ int opaque(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// exp(-2 pi i e / LR), 0 <= e < LR, LR a power of two: argument reduced to (-1/2, 1/2] rev.
+template <int LR>
+__device__ __forceinline__ float2 twiddle(int e) {
+  const float rev = (e > LR / 2) ? (float)(LR - e) * (1.0f / LR) : -(float)e * (1.0f / LR);
+  return make_float2(__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev));
+}
+
+// Twiddles of one radix-R group, w^m for w = exp(-2 pi i k / LR), m < R: the powers
+// w^1, w^2, w^4, w^8 are evaluated directly (v_sin/v_cos), every other power is a product
+// of at most log2(R) of them (<= 4 roundings), so a group holds log2(R) complex values.
+template <int R, int LR>
+struct GroupTwiddles {
+  static constexpr int NB = R == 2 ? 1 : R == 4 ? 2 : R == 8 ? 3 : 4;
+  float2 b[NB];
+  __device__ __forceinline__ void init(int k) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) b[i] = twiddle<LR>((k << i) & (LR - 1));
+  }
+  __device__ __forceinline__ float2 pow(int m) const {  // m compile-time after unrolling
+    float2 r = make_float2(1.f, 0.f);
+    bool first = true;
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      if ((m >> i) & 1) {
+        r = first ? b[i] : cmul(r, b[i]);
+        first = false;
+      }
+    return r;
+  }
+};
+
+// ---- small DFTs, natural order in and out -------------------------------------------
+__device__ __forceinline__ void dft2(float2& a, float2& b) {
+  const float2 t = a;
+  a = cadd(t, b);
+  b = csub(t, b);
+}
+
+__device__ __forceinline__ void dft4(float2& x0, float2& x1, float2& x2, float2& x3) {
+  const float2 a0 = cadd(x0, x2), a1 = csub(x0, x2);
+  const float2 a2 = cadd(x1, x3), a3 = mul_negi(csub(x1, x3));
+  x0 = cadd(a0, a2);
+  x2 = csub(a0, a2);
+  x1 = cadd(a1, a3);
+  x3 = csub(a1, a3);
+}
+
+template <int R> struct Dft;
+template <> struct Dft<2> {
+  __device__ __forceinline__ static void run(float2* v) { dft2(v[0], v[1]); }
+};
+template <> struct Dft<4> {
+  __device__ __forceinline__ static void run(float2* v) { dft4(v[0], v[1], v[2], v[3]); }
+};
+template <> struct Dft<8> {
+  __device__ __forceinline__ static void run(float2* v) {
+    // DIT: E = DFT4(even), O = DFT4(odd), X[k] = E[k] + w8^k O[k], X[k+4] = E[k] - w8^k O[k]
+    float2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
+    float2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
+    dft4(e0, e1, e2, e3);
+    dft4(o0, o1, o2, o3);
+    const float c = 0.70710678118654752440f;
+    const float2 t1 = make_float2(c * (o1.x + o1.y), c * (o1.y - o1.x));    // w8^1 o1
+    const float2 t2 = mul_negi(o2);                                          // w8^2 o2
+    const float2 t3 = make_float2(c * (o3.y - o3.x), -c * (o3.x + o3.y));   // w8^3 o3
+    v[0] = cadd(e0, o0); v[4] = csub(e0, o0);
+    v[1] = cadd(e1, t1); v[5] = csub(e1, t1);
+    v[2] = cadd(e2, t2); v[6] = csub(e2, t2);
+    v[3] = cadd(e3, t3); v[7] = csub(e3, t3);
+  }
+};
+template <> struct Dft<16> {
+  __device__ __forceinline__ static void run(float2* v) {
+    // N1 = N2 = 4, n = 4 n1 + n2, k = k1 + 4 k2:
+    //   Y[n2][k1] = DFT4_{n1}(x[4 n1 + n2]) * w16^{n2 k1};  X[k1 + 4 k2] = DFT4_{n2}(Y[n2][k1])
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) dft4(v[n2], v[n2 + 4], v[n2 + 8], v[n2 + 12]);
+    // after this, v[n2 + 4 k1] = Y[n2][k1]
+    const float c8 = 0.70710678118654752440f;   // cos(pi/4)
+    const float c16 = 0.92387953251128675613f;  // cos(pi/8)
+    const float s16 = 0.38268343236508977173f;  // sin(pi/8)
+    // w16^e = (cos(2 pi e/16), -sin(2 pi e/16))
+    v[5] = cmul(v[5], make_float2(c16, -s16));   // n2=1,k1=1: e=1
+    v[9] = cmul(v[9], make_float2(c8, -c8));     // n2=1,k1=2: e=2
+    v[13] = cmul(v[13], make_float2(s16, -c16)); // n2=1,k1=3: e=3
+    v[6] = cmul(v[6], make_float2(c8, -c8));     // n2=2,k1=1: e=2
+    v[10] = mul_negi(v[10]);                     // n2=2,k1=2: e=4
+    v[14] = cmul(v[14], make_float2(-c8, -c8));  // n2=2,k1=3: e=6
+    v[7] = cmul(v[7], make_float2(s16, -c16));   // n2=3,k1=1: e=3
+    v[11] = cmul(v[11], make_float2(-c8, -c8));  // n2=3,k1=2: e=6
+    v[15] = cmul(v[15], make_float2(-c16, s16)); // n2=3,k1=3: e=9
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) dft4(v[4 * k1], v[4 * k1 + 1], v[4 * k1 + 2], v[4 * k1 + 3]);
+    // now v[4 k1 + k2] = X[k1 + 4 k2]; transpose the 4x4 index to natural order
+    float2 t[16];
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1)
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) t[k1 + 4 * k2] = v[4 * k1 + k2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = t[i];
+  }
+};
+
+// Synchronisation between passes: an FFT that spans several waves needs a workgroup
+// barrier; inside one wave, LDS operations issue and complete in program order, and the
+// compiler keeps every read of a pass ahead of its (may-alias) writes.
+template <bool WG_SYNC>
+__device__ __forceinline__ void pass_sync() {
+  if constexpr (WG_SYNC) __syncthreads();
+  else __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+// One Stockham radix-R pass (L = size of the already-combined sub-transforms), in place on
+// `buf` (padded layout).  Thread t of P handles groups j = t + P g, g < 16/R.
+template <int N, int R, int L, int P, bool WG_SYNC>
+__device__ __forceinline__ void stockham_pass(float2* buf, int t) {
+  constexpr int G = N / R / P;
+  constexpr int S = N / R;
+  static_assert(G * R == 16, "16 values per thread");
+  float2 v[G][R];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const float2* src = buf + pad16(t + P * g);
+#pragma unroll
+    for (int m = 0; m < R; ++m) v[g][m] = src[padoff(m * S)];
+  }
+  pass_sync<WG_SYNC>();
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int j = t + P * g;
+    const int k = j & (L - 1);
+    if constexpr (L > 1) {
+      GroupTwiddles<R, L * R> tw;
+      tw.init(k);
+#pragma unroll
+      for (int m = 1; m < R; ++m) v[g][m] = cmul(v[g][m], tw.pow(m));
+    }
+    Dft<R>::run(v[g]);
+    float2* dst = buf + pad16((j / L) * L * R + k);
+#pragma unroll
+    for (int m = 0; m < R; ++m) dst[padoff(m * L)] = v[g][m];
+  }
+  pass_sync<WG_SYNC>();
+}
+
+// Passes L, L*R, ... up to N (all from LDS).
+template <int N, int L, int P, bool WG_SYNC>
+__device__ __forceinline__ void stockham_from(float2* buf, int t) {
+  if constexpr (L < N) {
+    constexpr int REM = N / L;
+    constexpr int R = REM >= 16 ? 16 : REM;
+    stockham_pass<N, R, L, P, WG_SYNC>(buf, t);
+    stockham_from<N, L * R, P, WG_SYNC>(buf, t);
+  }
+}
+
+// Radix of the last pass and the L it runs at, for the "last pass to registers" variant.
+template <int N> struct LastPass {
+  static constexpr int rem_after(int L) { return N / L; }
+  static constexpr int find_L() {
+    int L = 8;
+    while (N / L > 16) L *= 16;
+    return L;
+  }
+  static constexpr int Lp = find_L();
+  static constexpr int R = N / Lp;
+};
+
+// All passes after pass 0 except the last, which stays in registers: on return
+// out[g][m] holds X[d] for d = (t + P g) + m * (N / R) with R = LastPass<N>::R.
+template <int N, int L, int P, bool WG_SYNC>
+__device__ __forceinline__ void stockham_to_regs(float2* buf, int t, float2 (*out)[LastPass<N>::R]) {
+  constexpr int LP = LastPass<N>::Lp;
+  if constexpr (L < LP) {
+    constexpr int REM = N / L;
+    constexpr int R = REM >= 16 ? 16 : REM;
+    stockham_pass<N, R, L, P, WG_SYNC>(buf, t);
+    stockham_to_regs<N, L * R, P, WG_SYNC>(buf, t, out);
+  } else {
+    constexpr int R = LastPass<N>::R;
+    constexpr int G = N / R / P;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int j = t + P * g;
+      const float2* src = buf + pad16(j);
+#pragma unroll
+      for (int m = 0; m < R; ++m) out[g][m] = src[padoff(m * (N / R))];
+      GroupTwiddles<R, L * R> tw;
+      tw.init(j & (L - 1));
+#pragma unroll
+      for (int m = 1; m < R; ++m) out[g][m] = cmul(out[g][m], tw.pow(m));
+      Dft<R>::run(out[g]);
+    }
+  }
+}
+
+}  // namespace fmcw

@@ -1,0 +1,735 @@
+// fmcw_api.hip -- host side of libfmcw.so: the C-ABI declared in include/fmcw.h.
+//
+// The handle replaces the reference's elaborated radar_core instance (rtl/src/radar_core.vhd
+// generics :12-19, FFT IP configuration handshake cfg_proc :279-301): it validates the
+// configuration once, uploads the window tables (window_multiplier.vhd:34-49, as fp32) and
+// allocates every scratch buffer, so fmcw_enqueue only launches kernels (graph-capturable).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/fmcw.h"
+#include "kernels.hpp"
+
+using namespace fmcw;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char b[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(b, sizeof b, fmt, ap);
+  va_end(ap);
+  g_err = b;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                    \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess) return fail(FMCW_EHIP, "%s: %s (%s:%d)", #expr,               \
+                                      hipGetErrorString(e_), __FILE__, __LINE__);        \
+  } while (0)
+
+bool pow2(uint32_t x) { return x && !(x & (x - 1)); }
+
+struct PendingEvent {
+  int kid;
+  hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct fmcw_handle {
+  fmcw_config cfg{};
+  int n_cu = 256;
+  // range kernel geometry (runtime copies of RangeGeom<N>)
+  int T = 0, RB = 0, lgT = 0, lgRB = 0;
+  uint32_t chunk = 1;
+  // device buffers
+  float* win_r = nullptr;  // [ns]
+  float* win_d = nullptr;  // [nc]
+  float2* inter = nullptr; // chunk * nrx * ns * nc
+  float* lin_scratch = nullptr;  // chunk * ns * nc (2-D CFAR input when the caller wants no linear map)
+  fmcw_det* det_scratch = nullptr;
+  uint32_t det_scratch_cap = 0;
+  uint32_t* counter = nullptr;
+  uint32_t* wg_base = nullptr;
+  uint32_t* wg_count = nullptr;
+  uint32_t* wg_off = nullptr;
+  uint32_t* n_dets_tmp = nullptr;
+  size_t n_wg_max = 0;
+  // grid sizes
+  int grid_range = 0, grid_doppler = 0, grid_cfar = 0;
+  size_t cfar2d_smem = 0;
+  // profiling
+  bool profiling = false;
+  std::vector<PendingEvent> pending;
+  std::vector<hipEvent_t> free_events;
+  double ms[FMCW_K_COUNT] = {0, 0, 0, 0};
+  uint64_t launches[FMCW_K_COUNT] = {0, 0, 0, 0};
+};
+
+namespace {
+
+// ---- kernel dispatch tables ------------------------------------------------------------
+using RangeFn = void (*)(const void*, float2*, const float*, int, int);
+
+template <int N>
+RangeFn range_fn(int dtype) {
+  switch (dtype) {
+    case FMCW_IN_F32: return k_range<N, LoadF32>;
+    case FMCW_IN_F16: return k_range<N, LoadF16>;
+    case FMCW_IN_I16: return k_range<N, LoadI16>;
+  }
+  return nullptr;
+}
+
+struct RangeInfo {
+  RangeFn fn;
+  int T, RB, NT;
+};
+
+RangeInfo range_info(uint32_t n, int dtype) {
+  switch (n) {
+#define R_(N) case N: return {range_fn<N>(dtype), RangeGeom<N>::T, RangeGeom<N>::RB, RangeGeom<N>::NT};
+    R_(64) R_(128) R_(256) R_(512) R_(1024) R_(2048) R_(4096) R_(8192)
+#undef R_
+  }
+  return {nullptr, 0, 0, 0};
+}
+
+using DopplerFn = void (*)(const float2*, const float*, int, int, int, int, int, int, int, float*,
+                           float*, int, Cfar1DArgs, DetSink);
+struct DopplerInfo {
+  DopplerFn fn;
+  int RW, NT;
+};
+DopplerInfo doppler_info(uint32_t nc) {
+  switch (nc) {
+#define D_(N) case N: return {k_doppler<N>, DopplerGeom<N>::RW, DopplerGeom<N>::NT};
+    D_(32) D_(64) D_(128) D_(256) D_(512) D_(1024)
+#undef D_
+  }
+  return {nullptr, 0, 0};
+}
+
+using Cfar1Fn = void (*)(const float*, int, int, int, int, Cfar1DArgs, DetSink);
+Cfar1Fn cfar1_fn(uint32_t nc) {
+  switch (nc) {
+#define C_(N) case N: return k_cfar1d<N>;
+    C_(32) C_(64) C_(128) C_(256) C_(512) C_(1024)
+#undef C_
+  }
+  return nullptr;
+}
+
+using Cfar2Fn = void (*)(const float*, int, int, int, int, Cfar2DArgs, DetSink);
+struct Cfar2Info {
+  Cfar2Fn fn;
+  int TR;
+};
+Cfar2Info cfar2_info(uint32_t nc) {
+  switch (nc) {
+#define C_(N) case N: return {k_cfar2d<N>, Cfar2DGeom<N>::TR};
+    C_(32) C_(64) C_(128) C_(256) C_(512) C_(1024)
+#undef C_
+  }
+  return {nullptr, 0};
+}
+
+// 2-D CFAR derived parameters
+Cfar2DArgs cfar2_args(const fmcw_config& c) {
+  Cfar2DArgs a{};
+  a.gr = (int)c.cfar2d_guard_range;
+  a.gd = (int)c.cfar2d_guard_doppler;
+  a.hr = (int)(c.cfar2d_ref_range + c.cfar2d_guard_range);
+  a.hd = (int)(c.cfar2d_ref_doppler + c.cfar2d_guard_doppler);
+  a.n_ref = (2 * a.hr + 1) * (2 * a.hd + 1) - (2 * a.gr + 1) * (2 * a.gd + 1);
+  a.rank = std::min((int)((a.n_ref * (int)c.cfar2d_rank_pct) / 100), a.n_ref - 1);
+  a.sc_min = (float)c.cfar2d_scale_min;
+  a.sc_nom = (float)c.cfar2d_scale_nom;
+  a.sc_max = (float)c.cfar2d_scale_max;
+  a.override_ = (int)c.cfar2d_scale_override;
+  a.s_min = a.override_ ? (float)a.override_ : std::min(a.sc_min, std::min(a.sc_nom, a.sc_max));
+  return a;
+}
+
+Cfar1DArgs cfar1_args(const fmcw_config& c) {
+  Cfar1DArgs a{};
+  a.enabled = c.cfar_kind == FMCW_CFAR_OS1D;
+  a.ref = (int)c.cfar1d_ref;
+  a.guard = (int)c.cfar1d_guard;
+  a.rank = (int)c.cfar1d_rank;
+  a.alpha = c.cfar1d_alpha;
+  return a;
+}
+
+size_t cfar2_smem(uint32_t nc, int hr) {
+  switch (nc) {
+    case 32: return cfar2d_smem_bytes<32>(hr);
+    case 64: return cfar2d_smem_bytes<64>(hr);
+    case 128: return cfar2d_smem_bytes<128>(hr);
+    case 256: return cfar2d_smem_bytes<256>(hr);
+    case 512: return cfar2d_smem_bytes<512>(hr);
+    case 1024: return cfar2d_smem_bytes<1024>(hr);
+  }
+  return 0;
+}
+
+int validate(const fmcw_config& c) {
+  if (!pow2(c.n_range) || c.n_range < 64 || c.n_range > 8192)
+    return fail(FMCW_EINVAL, "n_range=%u: must be a power of two in [64, 8192]", c.n_range);
+  if (!pow2(c.n_doppler) || c.n_doppler < 32 || c.n_doppler > 1024)
+    return fail(FMCW_EINVAL, "n_doppler=%u: must be a power of two in [32, 1024]", c.n_doppler);
+  if (c.n_rx < 1 || c.n_rx > 64) return fail(FMCW_EINVAL, "n_rx=%u: must be in [1, 64]", c.n_rx);
+  if (c.in_dtype < FMCW_IN_F32 || c.in_dtype > FMCW_IN_I16)
+    return fail(FMCW_EINVAL, "in_dtype=%d unknown", c.in_dtype);
+  if (c.window != FMCW_WIN_NONE && c.window != FMCW_WIN_HAMMING)
+    return fail(FMCW_EINVAL, "window=%d unknown", c.window);
+  if (c.mag_mode != FMCW_MAG_ABS && c.mag_mode != FMCW_MAG_AMBM)
+    return fail(FMCW_EINVAL, "mag_mode=%d unknown", c.mag_mode);
+  if (c.mag_mode == FMCW_MAG_AMBM && c.n_rx != 1)
+    return fail(FMCW_EINVAL, "mag_mode AMBM is defined for n_rx == 1 only");
+  if (c.map_kind != FMCW_MAP_LINEAR && c.map_kind != FMCW_MAP_DB)
+    return fail(FMCW_EINVAL, "map_kind=%d unknown", c.map_kind);
+  if (range_info(c.n_range, c.in_dtype).T > (int)c.n_doppler)
+    return fail(FMCW_EINVAL, "n_doppler=%u smaller than the range kernel's chirp group", c.n_doppler);
+  if (c.max_frames < 1) return fail(FMCW_EINVAL, "max_frames must be >= 1");
+  if (c.cfar_kind == FMCW_CFAR_OS1D) {
+    if (c.cfar1d_ref < 1 || c.cfar1d_rank >= 2 * c.cfar1d_ref)
+      return fail(FMCW_EINVAL, "1-D CFAR: need ref >= 1 and rank < 2*ref");
+    if (2 * (c.cfar1d_ref + c.cfar1d_guard) + 1 > c.n_doppler)
+      return fail(FMCW_EINVAL, "1-D CFAR window wider than n_doppler");
+    if (!(c.cfar1d_alpha > 0.f)) return fail(FMCW_EINVAL, "1-D CFAR alpha must be > 0");
+  } else if (c.cfar_kind == FMCW_CFAR_OS2D) {
+    const Cfar2DArgs a = cfar2_args(c);
+    if (a.n_ref < 1 || a.n_ref > 128)
+      return fail(FMCW_EINVAL, "2-D CFAR: %d reference cells (supported 1..128)", a.n_ref);
+    if (2 * a.hd + 1 > (int)c.n_doppler)
+      return fail(FMCW_EINVAL, "2-D CFAR window wider than n_doppler");
+    if (c.cfar2d_scale_override > 7)
+      return fail(FMCW_EINVAL, "scale_override is a 3-bit port (0..7)");
+    if (cfar2_smem(c.n_doppler, a.hr) > 160 * 1024)
+      return fail(FMCW_EINVAL, "2-D CFAR range extent too large for LDS");
+  } else if (c.cfar_kind != FMCW_CFAR_NONE) {
+    return fail(FMCW_EINVAL, "cfar_kind=%d unknown", c.cfar_kind);
+  }
+  return FMCW_OK;
+}
+
+// fp32 window table: Hamming with the RTL's half-ROM mirrored address, computed in fp64
+// (window_multiplier.vhd:34-49, :97-102).  WIN_NONE uploads ones.
+std::vector<float> window_table(uint32_t n, int kind) {
+  std::vector<float> w(n, 1.0f);
+  if (kind == FMCW_WIN_HAMMING) {
+    const uint32_t half = n / 2;
+    for (uint32_t i = 0; i < n; ++i) {
+      uint32_t a = i < half ? i : n - 1 - i;
+      if (a > half - 1) a = half - 1;
+      w[i] = (float)(0.54 - 0.46 * std::cos(2.0 * M_PI * (double)a / (double)(n - 1)));
+    }
+  }
+  return w;
+}
+
+template <typename F>
+int occupancy_grid(F fn, int nt, size_t smem, int n_cu, int* grid) {
+  int per_cu = 0;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn),
+                                                              nt, smem);
+  if (e != hipSuccess || per_cu < 1) per_cu = 1;
+  *grid = per_cu * n_cu;
+  return FMCW_OK;
+}
+
+hipEvent_t take_event(fmcw_handle* h) {
+  if (!h->free_events.empty()) {
+    hipEvent_t e = h->free_events.back();
+    h->free_events.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+struct ProfScope {
+  fmcw_handle* h;
+  int kid;
+  hipStream_t s;
+  hipEvent_t a = nullptr;
+  ProfScope(fmcw_handle* h_, int kid_, hipStream_t s_) : h(h_), kid(kid_), s(s_) {
+    if (h->profiling) {
+      a = take_event(h);
+      if (a) hipEventRecord(a, s);
+    }
+  }
+  ~ProfScope() {
+    if (h->profiling && a) {
+      hipEvent_t b = take_event(h);
+      if (b) {
+        hipEventRecord(b, s);
+        h->pending.push_back({kid, a, b});
+      }
+    }
+  }
+};
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(FMCW_EHIP, "launch %s: %s", what, hipGetErrorString(e));
+  return FMCW_OK;
+}
+
+DetSink make_sink(fmcw_handle* h) {
+  DetSink s;
+  s.scratch = h->det_scratch;
+  s.cap = h->det_scratch_cap;
+  s.counter = h->counter;
+  s.wg_base = h->wg_base;
+  s.wg_count = h->wg_count;
+  return s;
+}
+
+size_t tiles_per_frame(const fmcw_handle* h) {
+  const fmcw_config& c = h->cfg;
+  if (c.cfar_kind == FMCW_CFAR_OS2D) {
+    const int tr = cfar2_info(c.n_doppler).TR;
+    return (c.n_range + tr - 1) / tr;
+  }
+  return c.n_range / doppler_info(c.n_doppler).RW;
+}
+
+// The CFAR launcher shared by fmcw_enqueue (map just produced by K2) and fmcw_cfar.
+int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipStream_t s) {
+  const fmcw_config& c = h->cfg;
+  const DetSink sink = make_sink(h);
+  const int tile0 = (int)(frame0 * tiles_per_frame(h));
+  if (c.cfar_kind == FMCW_CFAR_OS2D) {
+    const Cfar2Info ci = cfar2_info(c.n_doppler);
+    const int n_tiles = nf * (int)tiles_per_frame(h);
+    const int grid = std::min(n_tiles, h->grid_cfar);
+    ProfScope ps(h, FMCW_K_CFAR2D, s);
+    hipLaunchKernelGGL(ci.fn, dim3(grid), dim3(256), h->cfar2d_smem, s, map_chunk, (int)c.n_range,
+                       n_tiles, frame0, tile0, cfar2_args(c), sink);
+    return check_launch("k_cfar2d");
+  }
+  // 1-D on a caller map (fmcw_cfar); inside fmcw_enqueue the 1-D CFAR is fused into K2
+  const DopplerInfo di = doppler_info(c.n_doppler);
+  const int n_tiles = nf * (int)(c.n_range / di.RW);
+  const int grid = std::min(n_tiles, h->grid_doppler);
+  ProfScope ps(h, FMCW_K_CFAR2D, s);
+  hipLaunchKernelGGL(cfar1_fn(c.n_doppler), dim3(grid), dim3(di.NT), 0, s, map_chunk, (int)c.n_range,
+                     n_tiles, frame0, tile0, cfar1_args(c), sink);
+  return check_launch("k_cfar1d");
+}
+
+int launch_det_finish(fmcw_handle* h, size_t n_frames, fmcw_det* dets, size_t det_cap,
+                      uint32_t* n_dets_dev, hipStream_t s) {
+  const int n = (int)(n_frames * tiles_per_frame(h));
+  ProfScope ps(h, FMCW_K_COMPACT, s);
+  hipLaunchKernelGGL(k_det_scan, dim3(1), dim3(1024), 0, s, h->wg_count, h->wg_off, n, n_dets_dev);
+  int rc = check_launch("k_det_scan");
+  if (rc) return rc;
+  if (dets && det_cap) {
+    // entries past the handle's scratch capacity are never stored: clip to it as well
+    const uint32_t cap = (uint32_t)std::min<size_t>(det_cap, h->det_scratch_cap);
+    hipLaunchKernelGGL(k_det_copy, dim3((n + 255) / 256), dim3(256), 0, s, h->det_scratch,
+                       h->det_scratch_cap, h->wg_base, h->wg_count, h->wg_off, n, dets, cap);
+    rc = check_launch("k_det_copy");
+  }
+  return rc;
+}
+
+size_t cube_bytes(const fmcw_config& c, size_t n_frames) {
+  const size_t per = (size_t)c.n_rx * c.n_range * c.n_doppler;
+  const size_t eb = c.in_dtype == FMCW_IN_F32 ? 8 : 4;
+  return n_frames * per * eb;
+}
+
+bool is_device_ptr(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+}  // namespace
+
+// =======================================================================================
+extern "C" {
+
+const char* fmcw_version(void) { return "fmcw-mi355x 0.1.0 (gfx950)"; }
+int fmcw_abi_version(void) { return FMCW_ABI_VERSION; }
+const char* fmcw_last_error(void) { return g_err.c_str(); }
+
+void fmcw_config_default(fmcw_config* c) {
+  if (!c) return;
+  std::memset(c, 0, sizeof *c);
+  c->n_range = 1024;  // radar_core.vhd:13
+  c->n_doppler = 128; // :14
+  c->n_rx = 1;
+  c->in_dtype = FMCW_IN_F32;
+  c->window = FMCW_WIN_HAMMING;
+  c->mag_mode = FMCW_MAG_ABS;
+  c->map_kind = FMCW_MAP_LINEAR;
+  c->cfar_kind = FMCW_CFAR_OS2D;
+  c->cfar1d_ref = 8;  // rtl/old/radar_core_v3.vhd:376-380
+  c->cfar1d_guard = 2;
+  c->cfar1d_rank = 12;
+  c->cfar1d_alpha = 4.0f;
+  c->cfar2d_ref_range = 4;     // radar_core.vhd:16 CFAR_REF_R (rows)
+  c->cfar2d_guard_range = 1;   // :19 CFAR_GUARD_D=1 acts on rows (naming swap)
+  c->cfar2d_ref_doppler = 4;   // :17 CFAR_REF_D
+  c->cfar2d_guard_doppler = 2; // :18 CFAR_GUARD_R=2 acts along Doppler
+  c->cfar2d_rank_pct = 75;     // :380
+  c->cfar2d_scale_min = 2;
+  c->cfar2d_scale_nom = 4;
+  c->cfar2d_scale_max = 6;
+  c->cfar2d_scale_override = 0;
+  c->max_frames = 1;
+  c->chunk_frames = 0;
+  c->device_id = 0;
+}
+
+int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
+  if (!cfg || !out) return fail(FMCW_EINVAL, "null argument");
+  *out = nullptr;
+  int rc = validate(*cfg);
+  if (rc) return rc;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
+    (void)hipGetLastError();
+    return fail(FMCW_ENODEV, "no HIP device");
+  }
+  if (cfg->device_id < 0 || cfg->device_id >= ndev) return fail(FMCW_ENODEV, "device_id %d out of range", cfg->device_id);
+  HIP_TRY(hipSetDevice(cfg->device_id));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, cfg->device_id));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(FMCW_ENODEV, "device %d is %s; this build targets gfx950 (MI355X)", cfg->device_id,
+                prop.gcnArchName);
+
+  fmcw_handle* h = new fmcw_handle();
+  h->cfg = *cfg;
+  const fmcw_config& c = h->cfg;
+  h->n_cu = prop.multiProcessorCount;
+  const RangeInfo ri = range_info(c.n_range, c.in_dtype);
+  h->T = ri.T;
+  h->RB = ri.RB;
+  h->lgT = __builtin_ctz(ri.T);
+  h->lgRB = __builtin_ctz(ri.RB);
+  const size_t frame_inter = (size_t)c.n_rx * c.n_range * c.n_doppler * sizeof(float2);
+  if (c.chunk_frames) {
+    h->chunk = std::min<uint32_t>(c.chunk_frames, c.max_frames);
+  } else {
+    // keep the corner-turned intermediate of one chunk ~64 MiB (MALL-resident)
+    h->chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(c.max_frames, (64u << 20) / frame_inter));
+  }
+  auto cleanup = [&](int code) {
+    fmcw_destroy(h);
+    return code;
+  };
+#define ALLOC(ptr, bytes)                                                                   \
+  do {                                                                                      \
+    if (hipMalloc(reinterpret_cast<void**>(&(ptr)), (bytes)) != hipSuccess) {               \
+      (void)hipGetLastError();                                                              \
+      return cleanup(fail(FMCW_ENOMEM, "hipMalloc(%zu) for %s failed", (size_t)(bytes), #ptr)); \
+    }                                                                                       \
+  } while (0)
+  ALLOC(h->win_r, c.n_range * sizeof(float));
+  ALLOC(h->win_d, c.n_doppler * sizeof(float));
+  ALLOC(h->inter, h->chunk * frame_inter);
+  if (c.cfar_kind == FMCW_CFAR_OS2D) ALLOC(h->lin_scratch, (size_t)h->chunk * c.n_range * c.n_doppler * sizeof(float));
+  h->n_wg_max = (size_t)c.max_frames * tiles_per_frame(h);
+  h->det_scratch_cap = (uint32_t)std::min<size_t>((size_t)c.max_frames * 4096, 64u << 20);
+  ALLOC(h->det_scratch, (size_t)h->det_scratch_cap * sizeof(fmcw_det));
+  ALLOC(h->counter, 16);
+  ALLOC(h->n_dets_tmp, 16);
+  ALLOC(h->wg_base, h->n_wg_max * sizeof(uint32_t));
+  ALLOC(h->wg_count, h->n_wg_max * sizeof(uint32_t));
+  ALLOC(h->wg_off, h->n_wg_max * sizeof(uint32_t));
+#undef ALLOC
+  {
+    std::vector<float> wr = window_table(c.n_range, c.window), wd = window_table(c.n_doppler, c.window);
+    if (hipMemcpy(h->win_r, wr.data(), wr.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(h->win_d, wd.data(), wd.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(h->wg_count, 0, h->n_wg_max * sizeof(uint32_t)) != hipSuccess)
+      return cleanup(fail(FMCW_EHIP, "window upload failed"));
+  }
+  occupancy_grid(ri.fn, ri.NT, 0, h->n_cu, &h->grid_range);
+  const DopplerInfo di = doppler_info(c.n_doppler);
+  occupancy_grid(di.fn, di.NT, 0, h->n_cu, &h->grid_doppler);
+  if (c.cfar_kind == FMCW_CFAR_OS2D) {
+    const Cfar2DArgs a = cfar2_args(c);
+    h->cfar2d_smem = cfar2_smem(c.n_doppler, a.hr);
+    const Cfar2Info ci = cfar2_info(c.n_doppler);
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(ci.fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)h->cfar2d_smem) != hipSuccess)
+      (void)hipGetLastError();
+    occupancy_grid(ci.fn, 256, h->cfar2d_smem, h->n_cu, &h->grid_cfar);
+  }
+  *out = h;
+  return FMCW_OK;
+}
+
+int fmcw_destroy(fmcw_handle* h) {
+  if (!h) return FMCW_OK;
+  hipSetDevice(h->cfg.device_id);
+  void* ptrs[] = {h->win_r, h->win_d, h->inter, h->lin_scratch, h->det_scratch, h->counter,
+                  h->n_dets_tmp, h->wg_base, h->wg_count, h->wg_off};
+  for (void* p : ptrs)
+    if (p) hipFree(p);
+  for (auto& pe : h->pending) {
+    hipEventDestroy(pe.a);
+    hipEventDestroy(pe.b);
+  }
+  for (auto e : h->free_events) hipEventDestroy(e);
+  delete h;
+  return FMCW_OK;
+}
+
+int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_map, fmcw_det* dets,
+                 size_t det_cap, uint32_t* n_dets_dev, void* stream) {
+  if (!h || !cube) return fail(FMCW_EINVAL, "null handle or cube");
+  const fmcw_config& c = h->cfg;
+  if (n_frames < 1 || n_frames > c.max_frames)
+    return fail(FMCW_EINVAL, "n_frames=%zu outside [1, max_frames=%u]", n_frames, c.max_frames);
+  if (c.cfar_kind != FMCW_CFAR_NONE && !n_dets_dev)
+    return fail(FMCW_EINVAL, "n_dets_dev is required when a CFAR is configured");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const RangeInfo ri = range_info(c.n_range, c.in_dtype);
+  const DopplerInfo di = doppler_info(c.n_doppler);
+  const size_t frame_px = (size_t)c.n_range * c.n_doppler;
+  const size_t in_frame_bytes = cube_bytes(c, 1);
+  const Cfar1DArgs cf1 = cfar1_args(c);
+  const DetSink sink = make_sink(h);
+  int rc;
+  if (c.cfar_kind != FMCW_CFAR_NONE) HIP_TRY(hipMemsetAsync(h->counter, 0, sizeof(uint32_t), s));
+
+  for (size_t f0 = 0; f0 < n_frames; f0 += h->chunk) {
+    const int nf = (int)std::min<size_t>(h->chunk, n_frames - f0);
+    const void* src = static_cast<const char*>(cube) + f0 * in_frame_bytes;
+    {
+      const int n_groups = nf * (int)c.n_rx * (int)(c.n_doppler / ri.T);
+      ProfScope ps(h, FMCW_K_RANGE, s);
+      hipLaunchKernelGGL(ri.fn, dim3(std::min(n_groups, h->grid_range)), dim3(ri.NT), 0, s, src, h->inter,
+                         h->win_r, (int)c.n_doppler, n_groups);
+      if ((rc = check_launch("k_range"))) return rc;
+    }
+    float* lin = nullptr;
+    float* db = nullptr;
+    if (rd_map && c.map_kind == FMCW_MAP_LINEAR) lin = rd_map + f0 * frame_px;
+    if (rd_map && c.map_kind == FMCW_MAP_DB) db = rd_map + f0 * frame_px;
+    if (c.cfar_kind == FMCW_CFAR_OS2D && !lin) lin = h->lin_scratch;
+    {
+      const int n_tiles = nf * (int)(c.n_range / di.RW);
+      ProfScope ps(h, FMCW_K_DOPPLER, s);
+      hipLaunchKernelGGL(di.fn, dim3(std::min(n_tiles, h->grid_doppler)), dim3(di.NT), 0, s, h->inter,
+                         h->win_d, (int)c.n_range, (int)c.n_rx, h->lgT, h->lgRB, n_tiles, (int)f0,
+                         (int)(f0 * (c.n_range / di.RW)), lin, db, c.mag_mode, cf1, sink);
+      if ((rc = check_launch("k_doppler"))) return rc;
+    }
+    if (c.cfar_kind == FMCW_CFAR_OS2D) {
+      if ((rc = launch_cfar(h, lin, nf, (int)f0, s))) return rc;
+    }
+  }
+  if (c.cfar_kind != FMCW_CFAR_NONE) return launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, s);
+  return FMCW_OK;
+}
+
+int fmcw_process(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_map, fmcw_det* dets,
+                 size_t det_cap, size_t* n_dets, void* stream) {
+  if (!h || !cube) return fail(FMCW_EINVAL, "null handle or cube");
+  const fmcw_config& c = h->cfg;
+  if (n_frames < 1 || n_frames > c.max_frames)
+    return fail(FMCW_EINVAL, "n_frames=%zu outside [1, max_frames=%u]", n_frames, c.max_frames);
+  HIP_TRY(hipSetDevice(c.device_id));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const size_t cb = cube_bytes(c, n_frames);
+  const size_t map_bytes = n_frames * (size_t)c.n_range * c.n_doppler * sizeof(float);
+  void* d_cube = const_cast<void*>(cube);
+  float* d_map = rd_map;
+  fmcw_det* d_dets = dets;
+  std::vector<void*> owned;
+  auto release = [&]() {
+    for (void* p : owned) hipFree(p);
+  };
+  if (!is_device_ptr(cube)) {
+    HIP_TRY(hipMalloc(&d_cube, cb));
+    owned.push_back(d_cube);
+    if (hipMemcpyAsync(d_cube, cube, cb, hipMemcpyHostToDevice, s) != hipSuccess) {
+      release();
+      return fail(FMCW_EHIP, "cube upload failed");
+    }
+  }
+  if (rd_map && !is_device_ptr(rd_map)) {
+    if (hipMalloc(reinterpret_cast<void**>(&d_map), map_bytes) != hipSuccess) {
+      release();
+      return fail(FMCW_ENOMEM, "map scratch");
+    }
+    owned.push_back(d_map);
+  }
+  if (dets && det_cap && !is_device_ptr(dets)) {
+    if (hipMalloc(reinterpret_cast<void**>(&d_dets), det_cap * sizeof(fmcw_det)) != hipSuccess) {
+      release();
+      return fail(FMCW_ENOMEM, "det scratch");
+    }
+    owned.push_back(d_dets);
+  }
+  int rc = fmcw_enqueue(h, d_cube, n_frames, d_map, d_dets, det_cap, h->n_dets_tmp, stream);
+  if (rc) {
+    release();
+    return rc;
+  }
+  uint32_t nd = 0;
+  hipError_t e = hipSuccess;
+  if (c.cfar_kind != FMCW_CFAR_NONE)
+    e = hipMemcpyAsync(&nd, h->n_dets_tmp, sizeof nd, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess && rd_map && d_map != rd_map)
+    e = hipMemcpyAsync(rd_map, d_map, map_bytes, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess && dets && d_dets != dets && nd)
+    e = hipMemcpy(dets, d_dets, std::min<size_t>(nd, det_cap) * sizeof(fmcw_det), hipMemcpyDeviceToHost);
+  release();
+  if (e != hipSuccess) return fail(FMCW_EHIP, "fmcw_process: %s", hipGetErrorString(e));
+  if (n_dets) *n_dets = nd;
+  if (c.cfar_kind != FMCW_CFAR_NONE && (nd > det_cap || nd > h->det_scratch_cap))
+    return fail(FMCW_EDETCAP, "%u detections, det_cap %zu (handle limit %u)", nd, det_cap,
+                h->det_scratch_cap);
+  return FMCW_OK;
+}
+
+int fmcw_range_ct(fmcw_handle* h, const void* cube, size_t n_frames, void* spec, void* stream) {
+  if (!h || !cube || !spec) return fail(FMCW_EINVAL, "null argument");
+  const fmcw_config& c = h->cfg;
+  if (n_frames < 1 || n_frames > c.max_frames) return fail(FMCW_EINVAL, "n_frames out of range");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const RangeInfo ri = range_info(c.n_range, c.in_dtype);
+  const size_t in_frame_bytes = cube_bytes(c, 1);
+  const size_t fr_px = (size_t)c.n_rx * c.n_range * c.n_doppler;
+  for (size_t f0 = 0; f0 < n_frames; f0 += h->chunk) {
+    const int nf = (int)std::min<size_t>(h->chunk, n_frames - f0);
+    const int n_groups = nf * (int)c.n_rx * (int)(c.n_doppler / ri.T);
+    {
+      ProfScope ps(h, FMCW_K_RANGE, s);
+      hipLaunchKernelGGL(ri.fn, dim3(std::min(n_groups, h->grid_range)), dim3(ri.NT), 0, s,
+                         static_cast<const char*>(cube) + f0 * in_frame_bytes, h->inter, h->win_r,
+                         (int)c.n_doppler, n_groups);
+      int rc = check_launch("k_range");
+      if (rc) return rc;
+    }
+    const size_t total = (size_t)nf * fr_px;
+    hipLaunchKernelGGL(k_unblock, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, h->inter,
+                       static_cast<float2*>(spec) + f0 * fr_px, (int)c.n_range, (int)c.n_doppler, h->T,
+                       h->RB, total);
+    int rc = check_launch("k_unblock");
+    if (rc) return rc;
+  }
+  return FMCW_OK;
+}
+
+int fmcw_magnitude(const float* iq, float* out, size_t n, int mag_mode, void* stream) {
+  if (!iq || !out) return fail(FMCW_EINVAL, "null argument");
+  if (mag_mode != FMCW_MAG_ABS && mag_mode != FMCW_MAG_AMBM) return fail(FMCW_EINVAL, "mag_mode");
+  if (!n) return FMCW_OK;
+  hipLaunchKernelGGL(k_magnitude, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const float2*>(iq), out, n,
+                     mag_mode);
+  return check_launch("k_magnitude");
+}
+
+int fmcw_cfar(fmcw_handle* h, const float* map, size_t n_frames, fmcw_det* dets, size_t det_cap,
+              uint32_t* n_dets_dev, void* stream) {
+  if (!h || !map || !n_dets_dev) return fail(FMCW_EINVAL, "null argument");
+  const fmcw_config& c = h->cfg;
+  if (c.cfar_kind == FMCW_CFAR_NONE) return fail(FMCW_EINVAL, "handle has cfar_kind NONE");
+  if (n_frames < 1 || n_frames > c.max_frames) return fail(FMCW_EINVAL, "n_frames out of range");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  HIP_TRY(hipMemsetAsync(h->counter, 0, sizeof(uint32_t), s));
+  int rc = launch_cfar(h, map, (int)n_frames, 0, s);
+  if (rc) return rc;
+  return launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, s);
+}
+
+int fmcw_set_profiling(fmcw_handle* h, int enable) {
+  if (!h) return fail(FMCW_EINVAL, "null handle");
+  h->profiling = enable != 0;
+  return FMCW_OK;
+}
+
+int fmcw_kernel_times(fmcw_handle* h, double* ms, uint64_t* launches) {
+  if (!h) return fail(FMCW_EINVAL, "null handle");
+  for (auto& pe : h->pending) {
+    HIP_TRY(hipEventSynchronize(pe.b));
+    float t = 0.f;
+    HIP_TRY(hipEventElapsedTime(&t, pe.a, pe.b));
+    h->ms[pe.kid] += t;
+    h->launches[pe.kid] += 1;
+    h->free_events.push_back(pe.a);
+    h->free_events.push_back(pe.b);
+  }
+  h->pending.clear();
+  for (int k = 0; k < FMCW_K_COUNT; ++k) {
+    if (ms) ms[k] = h->ms[k];
+    if (launches) launches[k] = h->launches[k];
+  }
+  return FMCW_OK;
+}
+
+int fmcw_reset_kernel_times(fmcw_handle* h) {
+  if (!h) return fail(FMCW_EINVAL, "null handle");
+  int rc = fmcw_kernel_times(h, nullptr, nullptr);
+  for (int k = 0; k < FMCW_K_COUNT; ++k) {
+    h->ms[k] = 0;
+    h->launches[k] = 0;
+  }
+  return rc;
+}
+
+int fmcw_device_alloc(size_t bytes, void** ptr, int device_id) {
+  if (!ptr) return fail(FMCW_EINVAL, "null ptr");
+  HIP_TRY(hipSetDevice(device_id));
+  if (hipMalloc(ptr, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(FMCW_ENOMEM, "hipMalloc(%zu)", bytes);
+  }
+  return FMCW_OK;
+}
+
+int fmcw_device_free(void* ptr) {
+  if (ptr) HIP_TRY(hipFree(ptr));
+  return FMCW_OK;
+}
+
+int fmcw_memcpy(void* dst, const void* src, size_t bytes, int kind) {
+  const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost
+                                                                        : hipMemcpyDeviceToDevice;
+  HIP_TRY(hipMemcpy(dst, src, bytes, k));
+  return FMCW_OK;
+}
+
+int fmcw_device_count(int* n) {
+  if (!n) return fail(FMCW_EINVAL, "null");
+  *n = 0;
+  if (hipGetDeviceCount(n) != hipSuccess) {
+    (void)hipGetLastError();
+    *n = 0;
+  }
+  return FMCW_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,682 @@
+// kernels.hpp -- HIP kernels of the FMCW hot path for gfx950.
+//
+//  K1 k_range     window + range FFT + corner turn        (radar_core.vhd:267-327)
+//  K2 k_doppler   Doppler window + FFT + |X| / NCI + map + 1-D OS-CFAR
+//                                                        (radar_core.vhd:340-374, os_cfar.vhd)
+//  K3 k_cfar2d    2-D OS-CFAR over the magnitude map       (os_cfar_2d.vhd:83-230)
+//     k_det_scan / k_det_copy   deterministic detection list (radar_core.vhd:396-418)
+//
+// Intermediate (corner-turned range spectrum) layout in HBM, per (frame, rx):
+//     inter[rb][cb][RB][T]  complex fp32,  rb = r / RB, cb = c / T
+// where T = chirps per K1 workgroup and RB = 128 / T range bins, so K1 writes whole 1 KiB
+// chunks and K2 reads RW x T x 8 B contiguous runs; element (r, c) sits at
+//     ((rb * NCB + cb) * RB + r % RB) * T + c % T.
+// This is the corner turner's [range][chirp] order (corner_turner.vhd:80,
+// rd_addr = range + doppler * N_RANGE) tiled so both sides stream full lines.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+
+#include "../../include/fmcw.h"
+#include "fft_device.hpp"
+
+namespace fmcw {
+
+// --------------------------------------------------------------------------------------
+// Input loaders: two consecutive complex samples -> float4 (re0, im0, re1, im1).
+// ADC word {Q[31:16], I[15:0]} (rtl/src/tb_radar_core.vhd:115-118) = little-endian short2(I,Q).
+// --------------------------------------------------------------------------------------
+struct LoadF32 {
+  static constexpr int bytes = 8;
+  __device__ __forceinline__ static float4 load2(const void* base, size_t idx) {
+    return *reinterpret_cast<const float4*>(reinterpret_cast<const float2*>(base) + idx);
+  }
+};
+struct LoadF16 {
+  static constexpr int bytes = 4;
+  __device__ __forceinline__ static float4 load2(const void* base, size_t idx) {
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    const h4 h = *reinterpret_cast<const h4*>(reinterpret_cast<const uint32_t*>(base) + idx);
+    return make_float4((float)h[0], (float)h[1], (float)h[2], (float)h[3]);
+  }
+};
+struct LoadI16 {
+  static constexpr int bytes = 4;
+  __device__ __forceinline__ static float4 load2(const void* base, size_t idx) {
+    const short4 s = *reinterpret_cast<const short4*>(reinterpret_cast<const uint32_t*>(base) + idx);
+    return make_float4((float)s.x, (float)s.y, (float)s.z, (float)s.w);
+  }
+};
+
+// K1 geometry per range-FFT size: T chirps per workgroup, RB = 128/T (1 KiB chunks).
+template <int N> struct RangeGeom {
+  static constexpr int P = N / 16;                   // threads per transform
+  static constexpr int T = N <= 128 ? 32 : N <= 512 ? 16 : N == 1024 ? 8 : N == 2048 ? 4 : 2;
+  static constexpr int NT = T * P;                   // threads per workgroup
+  static constexpr int RB = 128 / T;                 // range bins per 1 KiB chunk
+  static constexpr int REG = padded(N) + 4;          // LDS row (complex) per chirp
+  static constexpr bool WG_SYNC = P > 64;            // transform spans several waves
+};
+
+// --------------------------------------------------------------------------------------
+// K1: window + range FFT + corner turn.  One workgroup = T chirps of one (frame, rx),
+// grid-stride over all chirp groups.  Each thread: 8 coalesced 16-B loads, windowing,
+// radix-8 pass in registers, Stockham passes through LDS, then the tiled transposed store.
+// --------------------------------------------------------------------------------------
+template <int N, typename LD>
+__global__ void __launch_bounds__(RangeGeom<N>::NT)
+k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* __restrict__ win,
+        int nc, int n_groups) {
+  using Gm = RangeGeom<N>;
+  constexpr int P = Gm::P, T = Gm::T, NT = Gm::NT, RB = Gm::RB, REG = Gm::REG;
+  __shared__ __attribute__((aligned(16))) float2 lds[T * REG];
+
+  const int tid = threadIdx.x;
+  const int q = tid / P;  // chirp within the group
+  const int t0 = tid % P;
+  const int ncb = nc / T;
+
+  // window coefficients for this thread's samples 2t + {0,1} + (N/8) m
+  float2 w[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) w[m] = *reinterpret_cast<const float2*>(win + 2 * t0 + (N / 8) * m);
+
+  // transposed-store geometry: piece i of this thread is range r0 + i*N/8, chirps c0, c0+1
+  const int e0 = 2 * tid;
+  const int chunk0 = e0 / (RB * T);
+  const int win0 = e0 - chunk0 * (RB * T);
+  const int r0 = chunk0 * RB + win0 / T;
+  const int c0 = win0 % T;
+  constexpr int CI = T * N / 1024;  // chunks advanced per piece
+  const int rd0_off = c0 * REG + pad16(r0);
+
+  int g = blockIdx.x;
+  float4 a[8];
+  if (g < n_groups) {
+    const int fr = g / ncb;
+    const size_t chirp = (size_t)fr * nc + (size_t)(g - fr * ncb) * T + q;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) a[m] = LD::load2(cube, chirp * N + 2 * t0 + (N / 8) * m);
+  }
+  for (; g < n_groups; g += gridDim.x) {
+    const int fr = g / ncb;  // frame*nrx + rx within this chunk
+    const int cb = g - fr * ncb;
+    const int t = opaque(t0);
+    float2* buf = lds + q * REG;
+
+    __syncthreads();  // previous group's transposed reads are done with lds
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      float2 v[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const float we = e ? w[m].y : w[m].x;
+        v[m] = e ? make_float2(a[m].z * we, a[m].w * we) : make_float2(a[m].x * we, a[m].y * we);
+      }
+      Dft<8>::run(v);
+      float2* d = buf + pad16((2 * t + e) * 8);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) d[m] = v[m];
+    }
+    // prefetch the next group into the (now free) input registers
+    {
+      const int gn = g + gridDim.x;
+      if (gn < n_groups) {
+        const int frn = gn / ncb;
+        const size_t chirp = (size_t)frn * nc + (size_t)(gn - frn * ncb) * T + q;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) a[m] = LD::load2(cube, chirp * N + 2 * t + (N / 8) * m);
+      }
+    }
+    pass_sync<Gm::WG_SYNC>();
+    stockham_from<N, 8, P, Gm::WG_SYNC>(buf, t);
+    __syncthreads();
+
+    // tiled corner turn: element (r, c) -> inter[rb][cb][RB][T]
+    const float2* rd0 = lds + opaque(rd0_off);
+    float2* dst = inter + (size_t)fr * N * nc + ((size_t)chunk0 * ncb + cb) * (RB * T) + win0;
+    const size_t dstep = (size_t)CI * ncb * (RB * T);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float2 v0, v1;
+      if constexpr ((N / 8) % 16 == 0) {
+        v0 = rd0[padoff(i * (N / 8))];
+        v1 = rd0[REG + padoff(i * (N / 8))];
+      } else {
+        v0 = lds[c0 * REG + pad16(r0 + i * (N / 8))];
+        v1 = lds[(c0 + 1) * REG + pad16(r0 + i * (N / 8))];
+      }
+      *reinterpret_cast<float4*>(dst + i * dstep) = make_float4(v0.x, v0.y, v1.x, v1.y);
+    }
+  }
+}
+
+// --------------------------------------------------------------------------------------
+// Detection sink shared by the CFAR kernels: per-workgroup atomic reservation in a scratch
+// list + (base, count) table; k_det_scan/k_det_copy then order the list by workgroup id,
+// which is (frame, range) order, so the result is deterministic.
+// --------------------------------------------------------------------------------------
+struct DetSink {
+  fmcw_det* scratch;
+  uint32_t cap;
+  uint32_t* counter;
+  uint32_t* wg_base;
+  uint32_t* wg_count;
+};
+
+template <int NT>
+__device__ __forceinline__ int block_excl_scan(int v, int* s_wave, int& total) {
+  constexpr int NW = NT / 64;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) s_wave[wv] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int i = 0; i < NW; ++i) {
+      const int tt = s_wave[i];
+      s_wave[i] = acc;
+      acc += tt;
+    }
+    s_wave[NW] = acc;
+  }
+  __syncthreads();
+  total = s_wave[NW];
+  const int r = s_wave[wv] + x - v;
+  __syncthreads();
+  return r;
+}
+
+struct Cfar1DArgs {
+  int enabled;
+  int ref, guard, rank;
+  float alpha;
+};
+
+// 1-D OS-CFAR along Doppler (circular) over an LDS block of RW magnitude rows (row stride
+// `rs` floats, index pad16(d)), plus ordered emission.  Thread (rr, t) tests cells
+// d = t + P i.  detect <=> #{refs : fl(alpha*ref) >= cut} < n_ref - rank, which is
+// cut > fl(alpha * sorted(refs)[rank]) (rtl/old/os_cfar.vhd:330-369) without a sort.
+template <int NC, int NT>
+__device__ __forceinline__ void cfar1d_emit(const float* mags, int rs, int rr, int t, int r0, int frame,
+                                            int wg, const Cfar1DArgs& cf, const DetSink& sink,
+                                            int* s_scan) {
+  constexpr int P = NC / 16;
+  constexpr int CELLS = NC / P;  // 16
+  const float* mrow = mags + rr * rs;
+  const int nref = 2 * cf.ref;
+  const int need = nref - cf.rank;
+  uint32_t bits = 0;
+#pragma unroll
+  for (int i = 0; i < CELLS; ++i) {
+    const int d = t + P * i;
+    const float cut = mrow[pad16(d)];
+    int cnt = 0;
+    for (int j = 1; j <= cf.ref; ++j) {
+      const float a = mrow[pad16((d - cf.guard - j) & (NC - 1))];
+      const float b = mrow[pad16((d + cf.guard + j) & (NC - 1))];
+      cnt += (cf.alpha * a >= cut) ? 1 : 0;
+      cnt += (cf.alpha * b >= cut) ? 1 : 0;
+    }
+    if (cnt < need) bits |= 1u << i;
+  }
+  int total;
+  const int excl = block_excl_scan<NT>(__popc(bits), s_scan, total);
+  if (threadIdx.x == 0) {
+    uint32_t base = 0;
+    if (total > 0) base = atomicAdd(sink.counter, (uint32_t)total);
+    sink.wg_base[wg] = base;
+    sink.wg_count[wg] = (uint32_t)total;
+    s_scan[NT / 64 + 1] = (int)base;
+  }
+  __syncthreads();
+  if (!bits) return;
+  const uint32_t base = (uint32_t)s_scan[NT / 64 + 1];
+  int o = excl;
+  for (int i = 0; i < CELLS; ++i) {
+    if (!((bits >> i) & 1u)) continue;
+    const int d = t + P * i;
+    const float cut = mrow[pad16(d)];
+    // exact ranked reference cell: the value with #less <= rank < #less_or_equal
+    float ranked = 0.f;
+    for (int j = 0; j < nref; ++j) {
+      const int oj = j < cf.ref ? -(cf.guard + 1 + j) : (cf.guard + 1 + j - cf.ref);
+      const float vj = mrow[pad16((d + oj) & (NC - 1))];
+      int lt = 0, le = 0;
+      for (int i2 = 0; i2 < nref; ++i2) {
+        const int o2 = i2 < cf.ref ? -(cf.guard + 1 + i2) : (cf.guard + 1 + i2 - cf.ref);
+        const float v2 = mrow[pad16((d + o2) & (NC - 1))];
+        lt += v2 < vj;
+        le += v2 <= vj;
+      }
+      if (lt <= cf.rank && cf.rank < le) ranked = vj;
+    }
+    const uint32_t slot = base + (uint32_t)o;
+    if (slot < sink.cap) {
+      fmcw_det dd;
+      dd.frame = (uint32_t)frame;
+      dd.range = (uint16_t)(r0 + rr);
+      dd.doppler = (uint16_t)d;
+      dd.mag = cut;
+      dd.threshold = cf.alpha * ranked;
+      sink.scratch[slot] = dd;
+    }
+    ++o;
+  }
+}
+
+// Stand-alone 1-D OS-CFAR over a caller-supplied [frame][range][doppler] map (fmcw_cfar).
+template <int NC>
+__global__ void __launch_bounds__((NC >= 1024 ? 4 : 4096 / NC) * (NC / 16))
+k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int tile0, Cfar1DArgs cf,
+         DetSink sink) {
+  constexpr int P = NC / 16;
+  constexpr int RW = NC >= 1024 ? 4 : 4096 / NC;
+  constexpr int NT = RW * P;
+  constexpr int REGM = padded(NC);
+  __shared__ __attribute__((aligned(16))) float mags[RW * REGM];
+  __shared__ int s_scan[NT / 64 + 2];
+  const int tid = threadIdx.x, rr = tid / P, t = tid % P;
+  const int tiles_per_frame = ns / RW;
+  for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const int f = tile / tiles_per_frame;
+    const int r0 = (tile - f * tiles_per_frame) * RW;
+    const float* src = map + ((size_t)f * ns + r0) * NC;
+    __syncthreads();
+    for (int e = tid; e < RW * NC; e += NT) {
+      const int rl = e / NC, d = e - rl * NC;
+      mags[rl * REGM + pad16(d)] = src[e];
+    }
+    __syncthreads();
+    cfar1d_emit<NC, NT>(mags, REGM, rr, t, r0, frame0 + f, tile0 + tile, cf, sink, s_scan);
+  }
+}
+
+// --------------------------------------------------------------------------------------
+// K2: Doppler window + FFT + magnitude (+NCI over rx) + map + 1-D OS-CFAR.
+// One workgroup = RW range bins x all NC chirps of one frame; grid-stride over tiles.
+// --------------------------------------------------------------------------------------
+template <int NC> struct DopplerGeom {
+  static constexpr int P = NC / 16;
+  static constexpr int RW = NC >= 1024 ? 4 : 256 / P;   // range bins per workgroup
+  static constexpr int NT = RW * P;
+  static constexpr int REGD = padded(NC) + 4;           // complex per range row in LDS
+  static constexpr int REGM = padded(NC);               // floats per range row (magnitudes)
+  static constexpr int LR = LastPass<NC>::R;
+  static constexpr int LG = 16 / LR;
+};
+
+template <int NC>
+__global__ void __launch_bounds__(DopplerGeom<NC>::NT)
+k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int ns, int nrx,
+          int lgT, int lgRB, int n_tiles, int frame0, int tile0, float* __restrict__ lin_map,
+          float* __restrict__ db_map, int mag_mode, Cfar1DArgs cf, DetSink sink) {
+  using Gm = DopplerGeom<NC>;
+  constexpr int P = Gm::P, RW = Gm::RW, NT = Gm::NT, REGD = Gm::REGD, REGM = Gm::REGM;
+  constexpr int LR = Gm::LR, LG = Gm::LG;
+  constexpr int PIECES = RW * NC / 2 / NT;  // 8 pieces of (r, c..c+1) per thread
+  __shared__ __attribute__((aligned(16))) float2 lds[RW * REGD];
+  __shared__ __attribute__((aligned(16))) float mags[RW * REGM];
+  __shared__ int s_scan[NT / 64 + 2];
+
+  const int rr = threadIdx.x / P;
+  const int tiles_per_frame = ns / RW;
+  const int T = 1 << lgT;
+  const int lgRWT = __builtin_ctz(RW) + lgT;
+  const int lgncb = __builtin_ctz(NC) - lgT;
+
+  for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const int tid = opaque(threadIdx.x);
+    const int t = tid % P;
+    float2* buf = lds + rr * REGD;
+    const int f = tile / tiles_per_frame;
+    const int r0 = (tile - f * tiles_per_frame) * RW;
+    float acc[LG][LR];
+#pragma unroll
+    for (int g = 0; g < LG; ++g)
+#pragma unroll
+      for (int m = 0; m < LR; ++m) acc[g][m] = 0.f;
+
+    for (int rx = 0; rx < nrx; ++rx) {
+      const float2* src = inter + ((size_t)f * nrx + rx) * (size_t)ns * NC;
+      // stage RW x NC complex from the tiled corner-turn layout, windowed on the way in
+      float4 x[PIECES];
+#pragma unroll
+      for (int i = 0; i < PIECES; ++i) {
+        const int e = 2 * (tid + NT * i);
+        const int cbi = e >> lgRWT;
+        const int wi = e & ((1 << lgRWT) - 1);
+        const int r = r0 + (wi >> lgT);
+        const int ci = wi & (T - 1);
+        const size_t off = ((((size_t)(r >> lgRB) << lgncb) + cbi) << lgRB | (r & ((1 << lgRB) - 1))) << lgT | ci;
+        x[i] = *reinterpret_cast<const float4*>(src + off);
+      }
+      __syncthreads();  // lds free (previous rx / tile done)
+#pragma unroll
+      for (int i = 0; i < PIECES; ++i) {
+        const int e = 2 * (tid + NT * i);
+        const int cbi = e >> lgRWT;
+        const int wi = e & ((1 << lgRWT) - 1);
+        const int rl = wi >> lgT;
+        const int c = (cbi << lgT) | (wi & (T - 1));
+        const float2 wv = *reinterpret_cast<const float2*>(win_d + c);
+        float2* d = lds + rl * REGD + pad16(c);  // c even: c, c+1 share a 16-block
+        d[0] = make_float2(x[i].x * wv.x, x[i].y * wv.x);
+        d[1] = make_float2(x[i].z * wv.y, x[i].w * wv.y);
+      }
+      __syncthreads();
+      stockham_from<NC, 1, P, false>(buf, t);  // NC <= 1024: one transform per wave
+#pragma unroll
+      for (int g = 0; g < LG; ++g) {
+        const float2* s0 = buf + pad16(t + P * g);
+#pragma unroll
+        for (int m = 0; m < LR; ++m) {
+          const float2 X = s0[padoff(m * (NC / LR))];
+          if (mag_mode == FMCW_MAG_AMBM) {
+            const float ai = fabsf(X.x), aq = fabsf(X.y);
+            const float mx = fmaxf(ai, aq), mn = fminf(ai, aq);
+            acc[g][m] = mx + floorf(mn * 0.25f) + floorf(mn * 0.125f);
+          } else {
+            acc[g][m] += X.x * X.x + X.y * X.y;
+          }
+        }
+      }
+    }
+    // magnitudes -> LDS (for the map store and the CFAR neighbourhood)
+    float* mrow = mags + rr * REGM;
+#pragma unroll
+    for (int g = 0; g < LG; ++g) {
+      float* m0 = mrow + pad16(t + P * g);
+#pragma unroll
+      for (int m = 0; m < LR; ++m)
+        m0[padoff(m * (NC / LR))] = (mag_mode == FMCW_MAG_AMBM) ? acc[g][m] : sqrtf(acc[g][m]);
+    }
+    __syncthreads();
+
+    // map store: RW*NC floats contiguous at [f][r0][0]
+    {
+      constexpr int Q = RW * NC / 4 / NT;
+      const size_t mbase = ((size_t)f * ns + r0) * NC;
+#pragma unroll
+      for (int i = 0; i < Q; ++i) {
+        const int e = 4 * (tid + NT * i);
+        const int rl = e / NC, d = e - rl * NC;
+        const float* mr = mags + rl * REGM + pad16(d);  // d % 4 == 0: 4 floats in one 16-block
+        const float4 v = make_float4(mr[0], mr[1], mr[2], mr[3]);
+        if (lin_map) *reinterpret_cast<float4*>(lin_map + mbase + e) = v;
+        if (db_map) {
+          const float k = 6.0205999132796239f;  // 20 / log2(10)
+          *reinterpret_cast<float4*>(db_map + mbase + e) =
+              make_float4(k * __log2f(v.x + 1.f), k * __log2f(v.y + 1.f), k * __log2f(v.z + 1.f),
+                          k * __log2f(v.w + 1.f));
+        }
+      }
+    }
+    if (cf.enabled)
+      cfar1d_emit<NC, NT>(mags, REGM, rr, t, r0, frame0 + f, tile0 + tile, cf, sink, s_scan);
+    __syncthreads();  // mags / lds reused by the next tile
+  }
+}
+
+// --------------------------------------------------------------------------------------
+// K3: 2-D OS-CFAR (rtl/src/os_cfar_2d.vhd:140-217) over the linear magnitude map.
+// One workgroup = TR CUT rows x all NC Doppler cells of one frame (Doppler circular);
+// the tile plus +-hr halo rows sits in LDS.  Wave w owns rows [w*TR/4, (w+1)*TR/4) so its
+// detections come out in (range, doppler) order.
+//
+// Phase A (one lane per cell): count c = #{refs : fl(s_min * ref) >= cut}.  Because
+// fl(s*x) is monotone in s and x, c >= n_ref - k proves cut <= fl(s * ranked) for every
+// admissible scale s >= s_min: the cell cannot detect.  Almost all noise cells stop here.
+// Phase B (whole wave per surviving cell): lanes hold refs l and l+64; mean from the fixed
+// fp32 halving tree (one add + xor-shuffles 32..1, = oracle tree_sum_f32); the scale
+// bracket from ballot counts (ranked > M <=> #{ref > M} >= n_ref - k; ranked < M' <=>
+// #{ref < M'} >= k + 1); detection <=> #{fl(s*ref) >= cut} < n_ref - k; for detections the
+// exact ranked value by a 32-step radix select on order-preserving keys.
+// --------------------------------------------------------------------------------------
+struct Cfar2DArgs {
+  int hr, gr, hd, gd;  // half extents (ref + guard) and guards, range / Doppler
+  int n_ref, rank;
+  float s_min, sc_min, sc_nom, sc_max;
+  int override_;
+};
+
+template <int NC> struct Cfar2DGeom {
+  static constexpr int NT = 256;
+  static constexpr int TR = 4096 / NC;   // CUT rows per workgroup (4096 cells)
+  static constexpr int CW = 4096 / 4;    // cells per wave
+};
+
+__device__ __forceinline__ uint32_t f2key(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+template <int NC>
+__global__ void __launch_bounds__(256)
+k_cfar2d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int tile0, Cfar2DArgs a,
+         DetSink sink) {
+  using Gm = Cfar2DGeom<NC>;
+  constexpr int TR = Gm::TR, CW = Gm::CW, NT = Gm::NT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  // carve: tile [(TR + 2 hr)][NC] | per-wave lists [4][CW] x (u32 cell, f32 thr) | offsets | scan
+  const int rows_in = TR + 2 * a.hr;
+  float* tile = smem;
+  uint2* lists = reinterpret_cast<uint2*>(smem + ((rows_in * NC + 3) & ~3));
+  short2* offs = reinterpret_cast<short2*>(lists + 4 * CW);
+  int* s_scan = reinterpret_cast<int*>(offs + 128);
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // reference-cell offsets in the fixed order (dr outer, dd inner, guard skipped)
+  if (tid == 0) {
+    int n = 0;
+    for (int dr = -a.hr; dr <= a.hr; ++dr)
+      for (int dd = -a.hd; dd <= a.hd; ++dd) {
+        if (abs(dr) <= a.gr && abs(dd) <= a.gd) continue;
+        offs[n++] = make_short2((short)dr, (short)dd);
+      }
+  }
+  const int need = a.n_ref - a.rank;
+  const int tiles_per_frame = (ns + TR - 1) / TR;
+
+  for (int tl = blockIdx.x; tl < n_tiles; tl += gridDim.x) {
+    const int f = tl / tiles_per_frame;
+    const int r0 = (tl - f * tiles_per_frame) * TR;
+    __syncthreads();
+    // load rows r0-hr .. r0+TR+hr-1 (zero outside the map)
+    const float* fm = map + (size_t)f * ns * NC;
+    for (int e = 4 * tid; e < rows_in * NC; e += 4 * NT) {
+      const int rl = e / NC;
+      const int r = r0 - a.hr + rl;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r >= 0 && r < ns) v = *reinterpret_cast<const float4*>(fm + (size_t)r * NC + (e - rl * NC));
+      *reinterpret_cast<float4*>(tile + e) = v;
+    }
+    __syncthreads();
+
+    // Phase A: survivors, as one 64-bit mask per 64-cell step of this wave's rows
+    constexpr int STEPS = CW / 64;
+    uint64_t surv[STEPS];
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s) {
+      const int cell = wv * CW + s * 64 + lane;
+      const int rl = cell / NC, d = cell - rl * NC;
+      const int r = r0 + rl;
+      bool sv = false;
+      if (r >= a.hr && r < ns - a.hr) {
+        const float* crow = tile + (rl + a.hr) * NC;
+        const float cut = crow[d];
+        int c = 0;
+        for (int dr = -a.hr; dr <= a.hr; ++dr) {
+          const float* row = crow + dr * NC;
+          const bool grow = abs(dr) <= a.gr;
+          for (int dd = -a.hd; dd <= a.hd; ++dd) {
+            if (grow && abs(dd) <= a.gd) continue;
+            c += (a.s_min * row[(d + dd) & (NC - 1)] >= cut) ? 1 : 0;
+          }
+        }
+        sv = c < need;
+      }
+      surv[s] = __ballot(sv);
+    }
+
+    // Phase B: whole-wave evaluation of each survivor, in cell order
+    int ndet = 0;
+    uint2* mylist = lists + wv * CW;
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s) {
+      uint64_t m = surv[s];
+      while (m) {
+        const int l0 = __builtin_ctzll(m);
+        m &= m - 1;
+        const int cell = wv * CW + s * 64 + l0;
+        const int rl = cell / NC, d = cell - rl * NC;
+        const float* crow = tile + (rl + a.hr) * NC;
+        const float cut = crow[d];
+        float va = 0.f, vb = 0.f;
+        const bool oka = lane < a.n_ref, okb = lane + 64 < a.n_ref;
+        if (oka) { const short2 o = offs[lane]; va = crow[o.x * NC + ((d + o.y) & (NC - 1))]; }
+        if (okb) { const short2 o = offs[lane + 64]; vb = crow[o.x * NC + ((d + o.y) & (NC - 1))]; }
+        float sum = va + vb;
+#pragma unroll
+        for (int x = 32; x >= 1; x >>= 1) sum += __shfl_xor(sum, x, 64);
+        const float mean = sum / (float)a.n_ref;
+        float sc;
+        if (a.override_) {
+          sc = (float)a.override_;
+        } else {
+          const float half = mean * 0.5f;
+          const float hi = mean + half;
+          const int n_hi = __popcll(__ballot(oka && va > hi)) + __popcll(__ballot(okb && vb > hi));
+          const int n_lo = __popcll(__ballot(oka && va < half)) + __popcll(__ballot(okb && vb < half));
+          sc = (n_hi >= need) ? a.sc_max : (n_lo >= a.rank + 1) ? a.sc_min : a.sc_nom;
+        }
+        const int n_ge = __popcll(__ballot(oka && sc * va >= cut)) + __popcll(__ballot(okb && sc * vb >= cut));
+        if (n_ge < need) {
+          // exact k-th smallest (k = rank) by radix select on order keys
+          const uint32_t ka = f2key(va), kb = f2key(vb);
+          uint32_t prefix = 0;
+          int k = a.rank;
+          for (int bit = 31; bit >= 0; --bit) {
+            const uint32_t hmask = bit == 31 ? 0u : ~((2u << bit) - 1u);
+            const bool za = oka && ((ka & hmask) == prefix) && !((ka >> bit) & 1u);
+            const bool zb = okb && ((kb & hmask) == prefix) && !((kb >> bit) & 1u);
+            const int c0 = __popcll(__ballot(za)) + __popcll(__ballot(zb));
+            if (k >= c0) { k -= c0; prefix |= 1u << bit; }
+          }
+          const float ranked = key2f(prefix);
+          if (lane == 0) mylist[ndet] = make_uint2((uint32_t)cell, __float_as_uint(sc * ranked));
+          ++ndet;
+        }
+      }
+    }
+    // ordered emission: waves in order, each list in cell order
+    int total;
+    const int excl = block_excl_scan<NT>(lane == 0 ? ndet : 0, s_scan, total);
+    const int wexcl = __shfl(excl, 0, 64);
+    if (tid == 0) {
+      uint32_t base = 0;
+      if (total > 0) base = atomicAdd(sink.counter, (uint32_t)total);
+      sink.wg_base[tile0 + tl] = base;
+      sink.wg_count[tile0 + tl] = (uint32_t)total;
+      s_scan[NT / 64 + 1] = (int)base;
+    }
+    __syncthreads();
+    const uint32_t base = (uint32_t)s_scan[NT / 64 + 1];
+    for (int i = lane; i < ndet; i += 64) {
+      const uint2 rec = mylist[i];
+      const uint32_t slot = base + (uint32_t)(wexcl + i);
+      if (slot < sink.cap) {
+        const int cell = (int)rec.x;
+        const int rl = cell / NC, d = cell - rl * NC;
+        fmcw_det dd;
+        dd.frame = (uint32_t)(frame0 + f);
+        dd.range = (uint16_t)(r0 + rl);
+        dd.doppler = (uint16_t)d;
+        dd.mag = tile[(rl + a.hr) * NC + d];
+        dd.threshold = __uint_as_float(rec.y);
+        sink.scratch[slot] = dd;
+      }
+    }
+  }
+}
+
+template <int NC>
+constexpr size_t cfar2d_smem_bytes(int hr) {
+  return (size_t)(((Cfar2DGeom<NC>::TR + 2 * hr) * NC + 3) & ~3) * 4 + 4 * Cfar2DGeom<NC>::CW * 8 +
+         128 * 4 + 16 * 4;
+}
+
+// --------------------------------------------------------------------------------------
+// Detection ordering: exclusive scan over per-workgroup counts (in workgroup = (frame,
+// range) order), then copy each workgroup's run to its final place.
+// --------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024)
+k_det_scan(const uint32_t* __restrict__ wg_count, uint32_t* __restrict__ wg_off, int n,
+           uint32_t* __restrict__ n_dets) {
+  __shared__ int s_wave[1024 / 64 + 2];
+  const int tid = threadIdx.x;
+  const int per = (n + 1023) / 1024;
+  const int b = tid * per;
+  const int e = min(b + per, n);
+  uint32_t s = 0;
+  for (int i = b; i < e; ++i) s += wg_count[i];
+  int total;
+  uint32_t run = (uint32_t)block_excl_scan<1024>((int)s, s_wave, total);
+  for (int i = b; i < e; ++i) {
+    wg_off[i] = run;
+    run += wg_count[i];
+  }
+  if (tid == 0) *n_dets = (uint32_t)total;
+}
+
+__global__ void k_det_copy(const fmcw_det* __restrict__ scratch, uint32_t scratch_cap,
+                           const uint32_t* __restrict__ wg_base, const uint32_t* __restrict__ wg_count,
+                           const uint32_t* __restrict__ wg_off, int n, fmcw_det* __restrict__ out,
+                           uint32_t cap) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t c = wg_count[i], b = wg_base[i], o = wg_off[i];
+  for (uint32_t k = 0; k < c; ++k)
+    if (b + k < scratch_cap && o + k < cap) out[o + k] = scratch[b + k];
+}
+
+// --------------------------------------------------------------------------------------
+// Utilities for the stage entry points.
+// --------------------------------------------------------------------------------------
+// inter (tiled) -> spec[fr][r][c] canonical corner-turner order.
+__global__ void k_unblock(const float2* __restrict__ inter, float2* __restrict__ spec, int ns, int nc,
+                          int T, int RB, size_t total) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const size_t per = (size_t)ns * nc;
+  const size_t fr = i / per;
+  const int rem = (int)(i - fr * per);
+  const int r = rem / nc, c = rem - r * nc;
+  const int ncb = nc / T;
+  const size_t off = ((size_t)((r / RB) * ncb + c / T) * RB + (r % RB)) * T + (c % T);
+  spec[i] = inter[fr * per + off];
+}
+
+__global__ void k_magnitude(const float2* __restrict__ iq, float* __restrict__ out, size_t n, int mode) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float2 X = iq[i];
+  if (mode == FMCW_MAG_AMBM) {
+    const float ai = fabsf(X.x), aq = fabsf(X.y);
+    const float mx = fmaxf(ai, aq), mn = fminf(ai, aq);
+    out[i] = mx + floorf(mn * 0.25f) + floorf(mn * 0.125f);
+  } else {
+    out[i] = sqrtf(X.x * X.x + X.y * X.y);
+  }
+}
+
+}  // namespace fmcw

@@ -1,0 +1,116 @@
+"""ctypes binding of libfmcw.so (include/fmcw.h).
+
+This is the binding a maintainer of the reference's Python tooling (model/) would add:
+plain ctypes over the C-ABI, no compiled Python extension.  The library is built in-tree
+(``make -C fpga-fmcw-radar-processor_amd``) and loaded from ``lib/libfmcw.so`` next to this
+package; it never falls back to anything else -- a missing library is an error.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+PKG_ROOT = Path(__file__).resolve().parent.parent          # fpga-fmcw-radar-processor_amd/
+LIB_PATH = Path(os.environ.get("FMCW_LIB", PKG_ROOT / "lib" / "libfmcw.so"))
+HEADER_PATH = PKG_ROOT.parent / "include" / "fmcw.h"
+
+# enums (fmcw.h)
+FMCW_OK, FMCW_EINVAL, FMCW_ENOMEM, FMCW_EHIP, FMCW_EDETCAP, FMCW_ENODEV = 0, -1, -2, -3, -4, -5
+IN_F32, IN_F16, IN_I16 = 0, 1, 2
+WIN_NONE, WIN_HAMMING = 0, 1
+MAG_ABS, MAG_AMBM = 0, 1
+MAP_LINEAR, MAP_DB = 1, 2
+CFAR_NONE, CFAR_OS1D, CFAR_OS2D = 0, 1, 2
+K_RANGE, K_DOPPLER, K_CFAR2D, K_COMPACT, K_COUNT = 0, 1, 2, 3, 4
+KERNEL_NAMES = ("k_range", "k_doppler", "k_cfar", "k_compact")
+
+STATUS_NAMES = {0: "FMCW_OK", -1: "FMCW_EINVAL", -2: "FMCW_ENOMEM", -3: "FMCW_EHIP",
+                -4: "FMCW_EDETCAP", -5: "FMCW_ENODEV"}
+
+
+class FmcwConfig(C.Structure):
+    _fields_ = [
+        ("n_range", C.c_uint32), ("n_doppler", C.c_uint32), ("n_rx", C.c_uint32),
+        ("in_dtype", C.c_int32), ("window", C.c_int32), ("mag_mode", C.c_int32),
+        ("map_kind", C.c_int32), ("cfar_kind", C.c_int32),
+        ("cfar1d_ref", C.c_uint32), ("cfar1d_guard", C.c_uint32), ("cfar1d_rank", C.c_uint32),
+        ("cfar1d_alpha", C.c_float),
+        ("cfar2d_ref_range", C.c_uint32), ("cfar2d_guard_range", C.c_uint32),
+        ("cfar2d_ref_doppler", C.c_uint32), ("cfar2d_guard_doppler", C.c_uint32),
+        ("cfar2d_rank_pct", C.c_uint32), ("cfar2d_scale_min", C.c_uint32),
+        ("cfar2d_scale_nom", C.c_uint32), ("cfar2d_scale_max", C.c_uint32),
+        ("cfar2d_scale_override", C.c_uint32),
+        ("max_frames", C.c_uint32), ("chunk_frames", C.c_uint32), ("device_id", C.c_int32),
+    ]
+
+
+class FmcwDet(C.Structure):
+    _fields_ = [("frame", C.c_uint32), ("range", C.c_uint16), ("doppler", C.c_uint16),
+                ("mag", C.c_float), ("threshold", C.c_float)]
+
+
+# every symbol include/fmcw.h declares, with its ctypes signature
+_VP, _SZ, _I, _U32P = C.c_void_p, C.c_size_t, C.c_int, C.POINTER(C.c_uint32)
+SIGNATURES = {
+    "fmcw_version": (C.c_char_p, []),
+    "fmcw_abi_version": (_I, []),
+    "fmcw_last_error": (C.c_char_p, []),
+    "fmcw_config_default": (None, [C.POINTER(FmcwConfig)]),
+    "fmcw_create": (_I, [C.POINTER(FmcwConfig), C.POINTER(_VP)]),
+    "fmcw_destroy": (_I, [_VP]),
+    "fmcw_enqueue": (_I, [_VP, _VP, _SZ, _VP, _VP, _SZ, _VP, _VP]),
+    "fmcw_process": (_I, [_VP, _VP, _SZ, _VP, _VP, _SZ, C.POINTER(_SZ), _VP]),
+    "fmcw_range_ct": (_I, [_VP, _VP, _SZ, _VP, _VP]),
+    "fmcw_magnitude": (_I, [_VP, _VP, _SZ, _I, _VP]),
+    "fmcw_cfar": (_I, [_VP, _VP, _SZ, _VP, _SZ, _VP, _VP]),
+    "fmcw_set_profiling": (_I, [_VP, _I]),
+    "fmcw_kernel_times": (_I, [_VP, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
+    "fmcw_reset_kernel_times": (_I, [_VP]),
+    "fmcw_device_alloc": (_I, [_SZ, C.POINTER(_VP), _I]),
+    "fmcw_device_free": (_I, [_VP]),
+    "fmcw_memcpy": (_I, [_VP, _VP, _SZ, _I]),
+    "fmcw_device_count": (_I, [C.POINTER(_I)]),
+}
+
+_lib = None
+
+
+class FmcwError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{STATUS_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+def load() -> C.CDLL:
+    """Load libfmcw.so (once).  Raises if it has not been built -- no fallback exists."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise FileNotFoundError(
+                f"{LIB_PATH} not built: run `make -C {PKG_ROOT}` or __graft_entry__.build()")
+        lib = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(code: int) -> int:
+    if code != FMCW_OK:
+        raise FmcwError(code, load().fmcw_last_error().decode(errors="replace"))
+    return code
+
+
+def default_config() -> FmcwConfig:
+    cfg = FmcwConfig()
+    load().fmcw_config_default(C.byref(cfg))
+    return cfg
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    load().fmcw_device_count(C.byref(n))
+    return n.value

@@ -1,0 +1,62 @@
+"""Text formats of the reference's simulation outputs, so model/ visualizers read our results.
+
+  detections  "r d mag" -- exactly 3 integer tokens per line (model/visualize_radar_targets.py:
+              117-120), searched under the names ADR_quick_det.txt / ADR_detections.txt
+              (:37-107); "quick" in the name selects the 128x32 geometry (:392-394).
+              Writer of record: the monitor process of rtl/old/tb_radar_core.vhd:173-208.
+  rd map      "r d 0 0 mag" -- 5 columns, range-major, as data/radar_output.txt.
+              The visualizer's parser rejects 5-token lines; this is the data/ format.
+  ADC input   "I Q" integer pairs, one sample per line, as data/golden_input_chirp.txt.
+"""
+from __future__ import annotations
+
+from pathlib import Path
+
+import numpy as np
+
+
+def write_detections(path, dets, frame: int | None = None) -> int:
+    """Write detections as 'r d mag' integer lines (optionally only one frame's)."""
+    d = dets if frame is None else dets[dets["frame"] == frame]
+    mag = np.rint(np.asarray(d["mag"], np.float64)).astype(np.int64)
+    with open(path, "w") as f:
+        for r, dd, m in zip(d["range"].tolist(), d["doppler"].tolist(), mag.tolist()):
+            f.write(f"{r} {dd} {m}\n")
+    return len(d)
+
+
+def read_detections(path) -> np.ndarray:
+    """Parse like load_detections() (visualize_radar_targets.py:109-122): 3-token lines only."""
+    rows = []
+    for line in Path(path).read_text().splitlines():
+        p = line.split()
+        if len(p) == 3:
+            rows.append([int(p[0]), int(p[1]), int(p[2])])
+    return np.array(rows, dtype=np.int64).reshape(-1, 3)
+
+
+def write_rd_map(path, rd_map: np.ndarray) -> None:
+    """One frame [range][doppler] -> 'r d 0 0 mag' lines, range-major, integer magnitudes."""
+    m = np.rint(np.asarray(rd_map, np.float64)).astype(np.int64)
+    nr, nd = m.shape
+    r = np.repeat(np.arange(nr), nd)
+    d = np.tile(np.arange(nd), nr)
+    z = np.zeros_like(r)
+    np.savetxt(path, np.stack([r, d, z, z, m.ravel()], axis=1), fmt="%d")
+
+
+def read_rd_map(path, n_range: int = 1024, n_doppler: int = 128) -> np.ndarray:
+    """data/radar_output.txt -> [range][doppler] int map (columns r d 0 0 mag)."""
+    a = np.loadtxt(path, dtype=np.int64)
+    out = np.zeros((n_range, n_doppler), np.int64)
+    out[a[:, 0], a[:, 1]] = a[:, 4]
+    return out
+
+
+def read_adc_pairs(path) -> np.ndarray:
+    """'I Q' integer lines (data/golden_input_chirp.txt) -> int array [n, 2]."""
+    return np.loadtxt(path, dtype=np.int64).reshape(-1, 2)
+
+
+def write_adc_pairs(path, iq: np.ndarray) -> None:
+    np.savetxt(path, np.asarray(iq, np.int64).reshape(-1, 2), fmt="%d")

@@ -1,0 +1,167 @@
+/*
+ * fmcw.h -- C-ABI of libfmcw.so, the MI355X (gfx950) FMCW range-Doppler + OS-CFAR
+ * hot path.  Plain C types only: pointers, sizes, enums.  No torch, no C++.
+ *
+ * What this boundary replaces in the reference (Aurellia-Beam/fpga-fmcw-radar-processor):
+ *
+ *   fmcw_config            radar_core generics  rtl/src/radar_core.vhd:12-19 and control
+ *                          ports mti_bypass / cfar_scale_ovr :47-49; FFT IP parameters
+ *                          vivado_proj/.../ip/xfft_0_1/xfft_0.xci:12-27 (size, direction,
+ *                          natural order); 1-D CFAR generics rtl/old/radar_core_v3.vhd:373-381
+ *   fmcw_create            the FFT-IP config handshake cfg_proc radar_core.vhd:279-301
+ *                          (config word x"0001" = forward, :247) -- done once per handle
+ *   fmcw_enqueue /         the radar_core AXI4-Stream entity radar_core.vhd:21-56: ADC words
+ *   fmcw_process           {Q[31:16], I[15:0]} in (:25-29), the Vivado IP calls
+ *                          u_range_fft / u_doppler_fft (:303-316, :351-364) and every stage
+ *                          between them (:267-390), detections out (:31-35, :396-418)
+ *   fmcw_det               det_tdata[16:0] / det_range_bin[9:0] / det_doppler_bin[6:0]
+ *                          (radar_core.vhd:31-35) + frame index + threshold (dbg_threshold,
+ *                          rtl/src/os_cfar_2d.vhd:34, :219)
+ *   FMCW_S_SATURATION etc. status_overflow (radar_core.vhd:447-456)
+ *   fmcw_range_ct          window_multiplier -> xfft_range -> corner_turner (:267-327),
+ *                          corner-turned spectrum as the CT emits it (corner_turner.vhd:80)
+ *   fmcw_magnitude         magnitude_calc (rtl/src/magnitude_calc.vhd:45-88)
+ *   fmcw_cfar              os_cfar_2d / os_cfar on a caller-supplied magnitude map
+ *                          (rtl/src/os_cfar_2d.vhd:83-230, rtl/old/os_cfar.vhd:295-380)
+ *
+ * Conventions
+ *   - Return value: 0 (FMCW_OK) or a negative fmcw_status.  fmcw_last_error() returns a
+ *     thread-local message for the last failure on the calling thread.
+ *   - fmcw_enqueue and the stage functions take DEVICE pointers only, are stream-ordered
+ *     and asynchronous (nothing synchronises, nothing allocates: graph-capturable).
+ *   - fmcw_process accepts host or device pointers (detected with hipPointerGetAttributes),
+ *     and returns after the results are in the caller's buffers.
+ *   - A handle is not thread-safe: one handle per host thread.  All scratch is allocated
+ *     at fmcw_create for up to cfg.max_frames frames per call.
+ *   - Layouts (row-major, complex = interleaved re,im):
+ *       cube   [frame][rx][chirp][sample]       in_dtype (f32 / f16 / int16 complex)
+ *       map    [frame][range][doppler]          float32 (range-major, as radar_output.txt)
+ *       spec   [frame][rx][range][chirp]        complex float32 (fmcw_range_ct)
+ *     Doppler bin 0 is zero Doppler (natural FFT order, no fftshift).
+ */
+#ifndef FMCW_H_
+#define FMCW_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FMCW_ABI_VERSION 1
+
+typedef enum {
+  FMCW_OK = 0,
+  FMCW_EINVAL = -1,       /* bad argument / unsupported configuration */
+  FMCW_ENOMEM = -2,       /* device allocation failed */
+  FMCW_EHIP = -3,         /* HIP runtime error (message in fmcw_last_error) */
+  FMCW_EDETCAP = -4,      /* detection list longer than det_cap; *n_dets = required count */
+  FMCW_ENODEV = -5        /* no usable gfx950 device */
+} fmcw_status;
+
+typedef enum { FMCW_IN_F32 = 0, FMCW_IN_F16 = 1, FMCW_IN_I16 = 2 } fmcw_in_dtype;
+typedef enum { FMCW_WIN_NONE = 0, FMCW_WIN_HAMMING = 1 } fmcw_window;
+/* FMCW_MAG_ABS: |X| = sqrt(re^2 + im^2) (with n_rx > 1: sqrt(sum_rx |X_rx|^2), NCI).
+ * FMCW_MAG_AMBM: max(|re|,|im|) + floor(min/4) + floor(min/8) (magnitude_calc.vhd:78-81). */
+typedef enum { FMCW_MAG_ABS = 0, FMCW_MAG_AMBM = 1 } fmcw_mag_mode;
+/* What fmcw_enqueue writes into rd_map: linear magnitude, or 20*log10(mag + 1). */
+typedef enum { FMCW_MAP_LINEAR = 1, FMCW_MAP_DB = 2 } fmcw_map_kind;
+typedef enum { FMCW_CFAR_NONE = 0, FMCW_CFAR_OS1D = 1, FMCW_CFAR_OS2D = 2 } fmcw_cfar_kind;
+
+typedef struct fmcw_config {
+  uint32_t n_range;        /* Ns: samples per chirp = range bins (N_RANGE); power of 2, 64..8192 */
+  uint32_t n_doppler;      /* Nc: chirps per frame = Doppler bins (N_DOPPLER); power of 2, 32..1024 */
+  uint32_t n_rx;           /* receive channels, >= 1; > 1 => non-coherent integration */
+  int32_t in_dtype;        /* fmcw_in_dtype */
+  int32_t window;          /* fmcw_window, applied on both fast and slow time */
+  int32_t mag_mode;        /* fmcw_mag_mode */
+  int32_t map_kind;        /* fmcw_map_kind */
+  int32_t cfar_kind;       /* fmcw_cfar_kind */
+  /* 1-D OS-CFAR along Doppler (circular): rtl/old/os_cfar.vhd generics */
+  uint32_t cfar1d_ref;     /* reference cells per side (REF_CELLS, 8) */
+  uint32_t cfar1d_guard;   /* guard cells per side (GUARD_CELLS, 2) */
+  uint32_t cfar1d_rank;    /* 0-based ascending rank k (RANK_IDX, 12) */
+  float cfar1d_alpha;      /* threshold multiplier (SCALING_MULT/SCALING_DIV, 4) */
+  /* 2-D OS-CFAR (rtl/src/os_cfar_2d.vhd), named by the axis each acts on (the RTL's
+   * GUARD_RANGE=2 acts along Doppler, GUARD_DOPPLER=1 along range) */
+  uint32_t cfar2d_ref_range;      /* 4 */
+  uint32_t cfar2d_guard_range;    /* 1 */
+  uint32_t cfar2d_ref_doppler;    /* 4 */
+  uint32_t cfar2d_guard_doppler;  /* 2 */
+  uint32_t cfar2d_rank_pct;       /* RANK_PCT 75 -> k = floor(n_ref*pct/100) */
+  uint32_t cfar2d_scale_min;      /* SCALE_MIN 2 */
+  uint32_t cfar2d_scale_nom;      /* SCALE_NOM 4 */
+  uint32_t cfar2d_scale_max;      /* SCALE_MAX 6 */
+  uint32_t cfar2d_scale_override; /* cfar_scale_ovr port; 0 = adaptive */
+  /* resources */
+  uint32_t max_frames;     /* largest n_frames per call (scratch is sized for it) */
+  uint32_t chunk_frames;   /* frames per internal kernel chunk (0 = auto) */
+  int32_t device_id;       /* HIP device ordinal */
+} fmcw_config;
+
+/* One detection: 16 bytes, sorted by (frame, range, doppler). */
+typedef struct fmcw_det {
+  uint32_t frame;
+  uint16_t range;
+  uint16_t doppler;
+  float mag;        /* CUT magnitude (det_tdata) */
+  float threshold;  /* scale * ranked reference cell (dbg_threshold) */
+} fmcw_det;
+
+typedef struct fmcw_handle fmcw_handle;
+
+/* Kernel ids for fmcw_kernel_times (profiling). */
+typedef enum {
+  FMCW_K_RANGE = 0,   /* window + range FFT + corner turn */
+  FMCW_K_DOPPLER = 1, /* Doppler window + FFT + magnitude (+NCI) (+1-D CFAR) + map */
+  FMCW_K_CFAR2D = 2,  /* 2-D OS-CFAR */
+  FMCW_K_COMPACT = 3, /* detection list ordering */
+  FMCW_K_COUNT = 4
+} fmcw_kernel_id;
+
+const char* fmcw_version(void);
+int fmcw_abi_version(void);
+const char* fmcw_last_error(void);
+
+/* Defaults = the reference core: N_RANGE 1024, N_DOPPLER 128, 1 rx, f32 in, Hamming,
+ * |X|, linear map, 2-D OS-CFAR with radar_core.vhd:376-382 parameters. */
+void fmcw_config_default(fmcw_config* cfg);
+
+int fmcw_create(const fmcw_config* cfg, fmcw_handle** out);
+int fmcw_destroy(fmcw_handle* h);
+
+/* Full hot path on n_frames frames, device pointers, asynchronous on `stream`
+ * (hipStream_t; NULL = default stream).  rd_map may be NULL.  dets may be NULL when
+ * cfar_kind == NONE.  *n_dets_dev (device uint32) receives the total detection count
+ * (which may exceed det_cap; entries beyond det_cap are dropped). */
+int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_map,
+                 fmcw_det* dets, size_t det_cap, uint32_t* n_dets_dev, void* stream);
+
+/* Synchronous convenience wrapper; pointers may be host or device memory. */
+int fmcw_process(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_map,
+                 fmcw_det* dets, size_t det_cap, size_t* n_dets, void* stream);
+
+/* Stage entry points (device pointers, asynchronous). */
+int fmcw_range_ct(fmcw_handle* h, const void* cube, size_t n_frames, void* spec, void* stream);
+int fmcw_magnitude(const float* iq, float* out, size_t n, int mag_mode, void* stream);
+int fmcw_cfar(fmcw_handle* h, const float* map, size_t n_frames, fmcw_det* dets,
+              size_t det_cap, uint32_t* n_dets_dev, void* stream);
+
+/* Profiling: when enabled, fmcw_enqueue brackets each kernel launch with hipEvents on
+ * its stream; fmcw_kernel_times synchronises and returns, per fmcw_kernel_id, the summed
+ * milliseconds and the number of launches since the last reset. */
+int fmcw_set_profiling(fmcw_handle* h, int enable);
+int fmcw_kernel_times(fmcw_handle* h, double* ms, uint64_t* launches);
+int fmcw_reset_kernel_times(fmcw_handle* h);
+
+/* Scratch-free helpers so callers without a device allocator can use the library. */
+int fmcw_device_alloc(size_t bytes, void** ptr, int device_id);
+int fmcw_device_free(void* ptr);
+int fmcw_memcpy(void* dst, const void* src, size_t bytes, int kind /*0 H2D,1 D2H,2 D2D*/);
+int fmcw_device_count(int* n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FMCW_H_ */

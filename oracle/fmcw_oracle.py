@@ -1,0 +1,330 @@
+"""CPU oracle for the FMCW range-Doppler + OS-CFAR hot path.
+
+TEST INFRASTRUCTURE ONLY.  This module is the *checker*: only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import it.
+The product path (``fpga-fmcw-radar-processor_amd/``) never imports, links or
+falls back to anything in ``oracle/``.
+
+What it restates (reference = Aurellia-Beam/fpga-fmcw-radar-processor, VHDL RTL):
+
+  stage                     reference (file:line)                         here
+  ------------------------  --------------------------------------------  -----------------------
+  ADC word {Q[31:16],I}     rtl/src/tb_radar_core.vhd:115-118             cube[..., chirp, sample]
+  Hamming window (half ROM) rtl/src/window_multiplier.vhd:34-49, 97-102   hamming_table()
+  Q15 window (compat)       rtl/src/window_multiplier.vhd:126-158         window_q15_rtl()
+  range FFT (fwd, natural)  rtl/src/radar_core.vhd:247, 303-316           range_ct()
+  corner turn               rtl/src/corner_turner.vhd:79-80               range_ct() (transpose)
+  Doppler window + FFT      rtl/src/radar_core.vhd:340-364                doppler_fft()
+  magnitude (AMBM compat)   rtl/src/magnitude_calc.vhd:57-81              ambm()
+  |X|, NCI, log-mag         SURVEY.md 8a-R7; model/visualize_radar_targets.py:468   magnitude(), log_mag()
+  1-D OS-CFAR 16/4          rtl/old/os_cfar.vhd:98-144, radar_core_v3.vhd:373-381   cfar_os1d()
+  2-D OS-CFAR 128 refs      rtl/src/os_cfar_2d.vhd:140-217, radar_core.vhd:376-382  cfar_os2d()
+  detection emission        rtl/src/radar_core.vhd:396-418                detections()
+
+Parity status (see DESIGN.md "Oracle"):
+  * The reference's FFT is the Xilinx LogiCORE FFT v9.1 (16-bit block floating
+    point, block exponent discarded at radar_core.vhd:310).  Its bit-accurate C
+    model may not be executed here (recorded denial), and no VHDL
+    simulator exists, so FFT *values* are pinned against the fp64 DFT definition
+    (numpy.fft) and the golden chirp's spectral peak, not against the IP:
+    "parity unpinned" at the IP boundary.
+  * Pinned by the reference's own known-answer tests / fixtures:
+    magnitude KAT (rtl/src/tb_magnitude_calc.vhd:49-73), corner-turn encode/decode
+    (rtl/src/tb_corner_turner.vhd:36-49,146-186), window endpoint/centre/symmetry
+    checks (rtl/src/tb_window_multiplier.vhd:182-240), the CFAR map
+    (rtl/src/tb_os_cfar_2d.vhd:52-75, ">= 2 detections"), the golden chirp
+    (data/golden_input_chirp.txt) and coarse invariants of data/radar_output.txt.
+
+The CFAR restatements here *sort* the reference cells literally, like the RTL
+bubble sort; the HIP kernels use an equivalent counting formulation, so the
+oracle is an independent check of that reformulation.  All CFAR arithmetic is
+float32 with a fixed, documented order so detections compare bit-exactly.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+import numpy as np
+
+# ---------------------------------------------------------------------------
+# Window
+# ---------------------------------------------------------------------------
+
+
+def hamming_table(n: int) -> np.ndarray:
+    """Hamming coefficients w[n] = 0.54 - 0.46 cos(2 pi i / (N-1)), fp64.
+
+    The RTL keeps only the first N/2 coefficients in a ROM and mirrors the
+    address for the second half (window_multiplier.vhd:40-42, :97-102), so the
+    table is exactly symmetric; for even N that equals the closed formula.
+    """
+    half = n // 2
+    idx = np.arange(n)
+    addr = np.where(idx < half, idx, n - 1 - idx)
+    addr = np.minimum(addr, max(half - 1, 0))  # :102 clamp (only matters for odd N)
+    return 0.54 - 0.46 * np.cos(2.0 * np.pi * addr / (n - 1))
+
+
+def hamming_q15(n: int) -> np.ndarray:
+    """Integer ROM contents c[i] = integer(w * 32767) (window_multiplier.vhd:43-46)."""
+    half = n // 2
+    w = 0.54 - 0.46 * np.cos(2.0 * np.pi * np.arange(half) / (n - 1))
+    c = np.floor(w * 32767.0 + 0.5).astype(np.int64)  # VHDL integer(real): round to nearest
+    return np.clip(c, 0, 32767)
+
+
+def window_q15_rtl(x: np.ndarray, n: int) -> np.ndarray:
+    """RTL-compat int16 window: y = sat16((x*c + 2^14) >> 14)  (window_multiplier.vhd:146-158).
+
+    Note the reference quirk: this is a 2x gain with a +1 LSB
+    bias, so a zero input yields 1.  Provenance only; the build's product path
+    is the fp32 window.
+    """
+    rom = hamming_q15(n)
+    half = n // 2
+    idx = np.arange(n)
+    addr = np.minimum(np.where(idx < half, idx, n - 1 - idx), half - 1)
+    c = rom[addr]
+    y = (x.astype(np.int64) * c + (1 << 14)) >> 14
+    return np.clip(y, -32768, 32767).astype(np.int64)
+
+
+# ---------------------------------------------------------------------------
+# FFT stages (fp64 reference; unscaled forward DFT, natural order)
+# ---------------------------------------------------------------------------
+
+
+def window_f32(n: int) -> np.ndarray:
+    """The exact fp32 window table the HIP path multiplies by."""
+    return hamming_table(n).astype(np.float32)
+
+
+def range_ct(cube: np.ndarray, window: bool = True) -> np.ndarray:
+    """Window + range FFT + corner turn.
+
+    cube: [..., chirp, sample] complex.  Returns [..., range, chirp] complex128:
+    X[r, c] = sum_n w[n] x[c, n] exp(-2 pi i r n / Ns) (forward, FWD_INV=1 at
+    radar_core.vhd:247; natural order, xfft_0.xci output ordering), then the
+    corner turn out[r][c] = in[c][r] (corner_turner.vhd:79-80).
+    """
+    x = cube.astype(np.complex128)
+    ns = x.shape[-1]
+    if window:
+        x = x * window_f32(ns).astype(np.float64)
+    return np.swapaxes(np.fft.fft(x, axis=-1), -1, -2)
+
+
+def doppler_fft(spec_rc: np.ndarray, window: bool = True) -> np.ndarray:
+    """Doppler window over slow time + forward Nc-point FFT per range bin (radar_core.vhd:340-364).
+
+    spec_rc: [..., range, chirp].  Returns [..., range, doppler]; bin 0 = zero
+    Doppler (natural order, no fftshift).
+    """
+    x = spec_rc.astype(np.complex128)
+    nc = x.shape[-1]
+    if window:
+        x = x * window_f32(nc).astype(np.float64)
+    return np.fft.fft(x, axis=-1)
+
+
+def magnitude(rd: np.ndarray, rx_axis: int | None = None) -> np.ndarray:
+    """|X| (fp64).  With rx_axis: non-coherent integration sqrt(sum_rx |X_rx|^2)."""
+    p = rd.real ** 2 + rd.imag ** 2
+    if rx_axis is not None:
+        p = p.sum(axis=rx_axis)
+    return np.sqrt(p)
+
+
+def log_mag(mag: np.ndarray) -> np.ndarray:
+    """20 log10(mag + 1), the visualizer's display transform (visualize_radar_targets.py:468)."""
+    return 20.0 * np.log10(mag + 1.0)
+
+
+def ambm(i, q):
+    """Alpha-max-beta-min |z| ~ max + floor(min/4) + floor(min/8) (magnitude_calc.vhd:57-81)."""
+    ai = np.abs(np.asarray(i, dtype=np.int64))
+    aq = np.abs(np.asarray(q, dtype=np.int64))
+    mx = np.maximum(ai, aq)
+    mn = np.minimum(ai, aq)
+    return mx + (mn >> 2) + (mn >> 3)
+
+
+# ---------------------------------------------------------------------------
+# OS-CFAR (float32, literal sort)
+# ---------------------------------------------------------------------------
+
+
+@dataclass
+class Cfar1D:
+    """1-D OS-CFAR along Doppler: rtl/old/os_cfar.vhd generics as instantiated at
+    rtl/old/radar_core_v3.vhd:373-381 (REF 8, GUARD 2, RANK 12, alpha 4/1)."""
+    ref: int = 8
+    guard: int = 2
+    rank: int = 12
+    alpha: float = 4.0
+
+
+@dataclass
+class Cfar2D:
+    """2-D OS-CFAR: rtl/src/os_cfar_2d.vhd as instantiated at radar_core.vhd:376-382.
+
+    Axis naming follows what each generic *does* in the RTL:
+    the line-buffer rows are range bins, the shift positions Doppler bins, so
+    the reference's GUARD_RANGE=2 acts along Doppler and GUARD_DOPPLER=1 along
+    range.  Defaults reproduce the reference window: 11 range rows x 13 Doppler
+    cells, guard 3 x 5, 128 reference cells, rank floor(128*75/100) = 96.
+    """
+    ref_range: int = 4
+    guard_range: int = 1
+    ref_doppler: int = 4
+    guard_doppler: int = 2
+    rank_pct: int = 75
+    scale_min: int = 2
+    scale_nom: int = 4
+    scale_max: int = 6
+    scale_override: int = 0
+
+    @property
+    def n_ref(self) -> int:
+        wr = 2 * (self.ref_range + self.guard_range) + 1
+        wd = 2 * (self.ref_doppler + self.guard_doppler) + 1
+        return wr * wd - (2 * self.guard_range + 1) * (2 * self.guard_doppler + 1)
+
+    @property
+    def rank(self) -> int:
+        k = (self.n_ref * self.rank_pct) // 100  # os_cfar_2d.vhd:181-182
+        return min(k, self.n_ref - 1)
+
+
+def cfar_os1d(mag: np.ndarray, p: Cfar1D = Cfar1D()):
+    """1-D OS-CFAR along the last (Doppler) axis, circular.
+
+    Refs: p.ref cells each side beyond p.guard guard cells (os_cfar.vhd:330-341),
+    sorted ascending (:349-357), T = alpha * refs[rank] (:364), detect CUT > T
+    (:369).  Build spec differences: circular in Doppler, no
+    17-bit truncation of T, fp32 arithmetic.
+
+    Returns (det mask bool, threshold float32) with mag's shape.
+    """
+    m = np.asarray(mag, dtype=np.float32)
+    offs = [-(p.guard + 1 + i) for i in range(p.ref)] + [p.guard + 1 + i for i in range(p.ref)]
+    refs = np.stack([np.roll(m, -o, axis=-1) for o in offs])  # refs[j][..., d] = m[..., d+o_j]
+    refs.sort(axis=0)
+    thr = (np.float32(p.alpha) * refs[p.rank]).astype(np.float32)
+    return m > thr, thr
+
+
+def cfar2d_offsets(p: Cfar2D):
+    """Reference-cell offsets (dr, dd) in the fixed summation order: dr ascending
+    (outer), dd ascending (inner), guard block skipped (os_cfar_2d.vhd:155-167)."""
+    hr = p.ref_range + p.guard_range
+    hd = p.ref_doppler + p.guard_doppler
+    out = []
+    for dr in range(-hr, hr + 1):
+        for dd in range(-hd, hd + 1):
+            if abs(dr) <= p.guard_range and abs(dd) <= p.guard_doppler:
+                continue
+            out.append((dr, dd))
+    return out
+
+
+def tree_sum_f32(refs: np.ndarray) -> np.ndarray:
+    """Sum over axis 0 in the build's fixed fp32 order: pad with zeros to 128 (adding 0
+    is exact), then halve: s[i] = x[i] + x[i + n/2] until one term remains.  The RTL
+    sums exact integers (os_cfar_2d.vhd:163); fp32 needs *an* order, and this one is
+    what a wave computes with one add per lane followed by xor-shuffles 32..1."""
+    x = np.asarray(refs, dtype=np.float32)
+    n = x.shape[0]
+    assert n <= 128
+    if n < 128:
+        x = np.concatenate([x, np.zeros((128 - n,) + x.shape[1:], np.float32)])
+    while x.shape[0] > 1:
+        h = x.shape[0] // 2
+        x = (x[:h] + x[h:]).astype(np.float32)
+    return x[0]
+
+
+def cfar_os2d(mag: np.ndarray, p: Cfar2D = Cfar2D()):
+    """2-D OS-CFAR over a [range, doppler] map (fp32), Doppler circular.
+
+    Per CUT (os_cfar_2d.vhd:152-217): the n_ref reference cells are sorted
+    ascending and ranked = refs[rank]; mean = tree_sum_f32(refs in cfar2d_offsets()
+    order) / n_ref; scale = override if nonzero, else scale_max
+    if ranked > mean + mean/2, scale_min if ranked < mean/2, else scale_nom;
+    detect if CUT > fl32(ranked * scale).  Range edges: a CUT is tested only when
+    its whole range extent lies inside the map (build spec).
+
+    Returns (det mask bool, threshold float32); threshold is 0 on untested rows.
+    """
+    m = np.asarray(mag, dtype=np.float32)
+    nr, nd = m.shape
+    hr = p.ref_range + p.guard_range
+    offs = cfar2d_offsets(p)
+    det = np.zeros((nr, nd), dtype=bool)
+    thr_out = np.zeros((nr, nd), dtype=np.float32)
+    if nr < 2 * hr + 1:
+        return det, thr_out
+    rows = np.arange(hr, nr - hr)
+    refs = np.empty((len(offs), rows.size, nd), dtype=np.float32)
+    for j, (dr, dd) in enumerate(offs):
+        refs[j] = np.roll(m[rows + dr], -dd, axis=-1)
+    mean = (tree_sum_f32(refs) / np.float32(len(offs))).astype(np.float32)
+    refs.sort(axis=0)
+    ranked = refs[p.rank]
+    if p.scale_override:
+        scale = np.full(ranked.shape, p.scale_override, dtype=np.float32)
+    else:
+        half = (mean * np.float32(0.5)).astype(np.float32)
+        hi = (mean + half).astype(np.float32)
+        scale = np.where(ranked > hi, np.float32(p.scale_max),
+                         np.where(ranked < half, np.float32(p.scale_min), np.float32(p.scale_nom)))
+    thr = (ranked * scale.astype(np.float32)).astype(np.float32)
+    det[rows] = m[rows] > thr
+    thr_out[rows] = thr
+    return det, thr_out
+
+
+DET_DTYPE = np.dtype([("frame", "<u4"), ("range", "<u2"), ("doppler", "<u2"),
+                      ("mag", "<f4"), ("threshold", "<f4")])
+
+
+def detections(det: np.ndarray, mag: np.ndarray, thr: np.ndarray, frame: int = 0) -> np.ndarray:
+    """Detection list in range-major scan order (radar_core.vhd:396-418: index
+    counters walk range-major, emit only non-zero CFAR outputs)."""
+    r, d = np.nonzero(det)
+    out = np.empty(r.size, dtype=DET_DTYPE)
+    out["frame"] = frame
+    out["range"] = r
+    out["doppler"] = d
+    out["mag"] = np.asarray(mag, dtype=np.float32)[r, d]
+    out["threshold"] = thr[r, d]
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Whole pipeline
+# ---------------------------------------------------------------------------
+
+
+def process(cube: np.ndarray, cfar=None, window: bool = True):
+    """Full hot path for one frame.
+
+    cube: [rx, chirp, sample] (or [chirp, sample]) complex.  Returns dict with the
+    fp64 map 'mag' [range, doppler], the float32 map used by the CFAR, the
+    detection mask and the detection list.  With several rx channels the map is
+    the non-coherent integration sqrt(sum_rx |X|^2).
+    """
+    c = np.asarray(cube)
+    if c.ndim == 2:
+        c = c[None]
+    rd = doppler_fft(range_ct(c, window), window)  # [rx, range, doppler]
+    mag = magnitude(rd, rx_axis=0)
+    mag32 = mag.astype(np.float32)
+    if cfar is None:
+        det = np.zeros(mag.shape, bool)
+        thr = np.zeros(mag.shape, np.float32)
+    elif isinstance(cfar, Cfar1D):
+        det, thr = cfar_os1d(mag32, cfar)
+    else:
+        det, thr = cfar_os2d(mag32, cfar)
+    return {"rd": rd, "mag": mag, "mag32": mag32, "det": det, "thr": thr,
+            "dets": detections(det, mag32, thr)}

@@ -1,0 +1,286 @@
+"""GPU parity: libfmcw.so (HIP, gfx950) vs the CPU oracle on identical inputs.
+
+Tolerances (BASELINE.json north_star; SURVEY.md 7 "Hard parts"):
+  * FFT values / maps: per frame max|gpu - ref| / max|ref| <= 1e-4, plus per-bin relative
+    error <= 1e-4 on bins above 1e-3 of the frame peak.  (fp32 vs fp64 reference.)
+  * detections: bit-exact -- indices, magnitude and threshold -- when the oracle CFAR runs on
+    the GPU's own float32 map (stage exactness).  Against the fp64 end-to-end oracle, the
+    lists agree except cells whose |cut - threshold| / threshold < 1e-4 (decided by fp32
+    rounding of the FFT, not by the CFAR).
+"""
+import ctypes as C
+import json
+
+import numpy as np
+import pytest
+
+import fmcw_oracle as O
+from conftest import GOLDEN, rel_err
+from fmcw import RadarCore, DeviceBuffer, DET_DTYPE, magnitude, synth
+
+pytestmark = pytest.mark.gpu
+
+MAP_TOL = 1e-4
+
+
+def check_map(gpu, ref, tol=MAP_TOL):
+    for f in range(ref.shape[0]):
+        e = rel_err(gpu[f], ref[f])
+        assert e <= tol, f"frame {f}: max rel err {e:.3g}"
+        big = np.abs(ref[f]) >= 1e-3 * np.abs(ref[f]).max()
+        pb = np.max(np.abs(gpu[f][big] - ref[f][big]) / np.abs(ref[f][big]))
+        assert pb <= tol, f"frame {f}: per-bin rel err {pb:.3g}"
+
+
+def to_complex(cube, dtype):
+    if dtype == "f32":
+        return cube.astype(np.complex128)
+    x = cube.astype(np.float64)
+    return x[..., 0] + 1j * x[..., 1]
+
+
+def run_range_ct(core, cube, nf):
+    c = core.cfg
+    din = DeviceBuffer(cube.nbytes)
+    din.upload(cube)
+    spec = DeviceBuffer(nf * c.n_rx * c.n_range * c.n_doppler * 8)
+    core.range_ct(din, spec, nf)
+    return spec.download(np.complex64, (nf, c.n_rx, c.n_range, c.n_doppler))
+
+
+def run_cfar_stage(core, mag, cap=1 << 16):
+    nf = mag.shape[0]
+    dm = DeviceBuffer(mag.nbytes)
+    dm.upload(np.ascontiguousarray(mag, np.float32))
+    dd = DeviceBuffer(cap * 16)
+    dn = DeviceBuffer(16)
+    core.cfar(dm, nf, dd, cap, dn)
+    n = int(dn.download(np.uint32, (1,))[0])
+    assert n <= cap
+    return dd.download(DET_DTYPE, (cap,))[:n]
+
+
+def oracle_dets(mag32, cfar):
+    out = []
+    for f in range(mag32.shape[0]):
+        if isinstance(cfar, O.Cfar1D):
+            det, thr = O.cfar_os1d(mag32[f], cfar)
+        else:
+            det, thr = O.cfar_os2d(mag32[f], cfar)
+        out.append(O.detections(det, mag32[f], thr, frame=f))
+    return np.concatenate(out) if out else np.empty(0, O.DET_DTYPE)
+
+
+# ------------------------------------------------------------------------------------------
+def test_magnitude_kat_gpu(gpu):
+    """magnitude_calc KAT (tb_magnitude_calc.vhd:49-73) through fmcw_magnitude, AMBM mode."""
+    kat = json.loads((GOLDEN / "mag_kat.json").read_text())
+    iq = np.array([[k["i"], k["q"]] for k in kat], np.float32)
+    di = DeviceBuffer(iq.nbytes)
+    di.upload(iq)
+    do = DeviceBuffer(len(kat) * 4)
+    magnitude(di, do, len(kat), "ambm")
+    got = do.download(np.float32, (len(kat),))
+    np.testing.assert_array_equal(got.astype(np.int64), [k["expect"] for k in kat])
+    magnitude(di, do, len(kat), "abs")
+    got = do.download(np.float32, (len(kat),))
+    np.testing.assert_allclose(got, np.hypot(iq[:, 0], iq[:, 1]), rtol=2e-7)
+
+
+@pytest.mark.parametrize("ns,nc,nrx,dtype,nf", [
+    (256, 128, 1, "f32", 2),      # config 1 geometry
+    (1024, 256, 1, "f32", 3),     # config 2 geometry
+    (1024, 128, 1, "i16", 2),     # reference core N_RANGE x N_DOPPLER, ADC ints
+    (4096, 64, 2, "f32", 1),
+    (8192, 32, 1, "f16", 1),      # largest range FFT, fp16 samples
+    (64, 32, 1, "f32", 4),        # smallest
+    (128, 64, 1, "i16", 2),
+    (512, 64, 1, "f32", 2),
+    (2048, 32, 1, "f16", 2),
+])
+def test_range_ct_parity(gpu, ns, nc, nrx, dtype, nf):
+    """window + range FFT + corner turn vs oracle range_ct (fp64)."""
+    rng = np.random.default_rng(ns + nc)
+    if dtype == "f32":
+        cube = (rng.uniform(-3e4, 3e4, (nf, nrx, nc, ns)) + 1j * rng.uniform(-3e4, 3e4, (nf, nrx, nc, ns))).astype(np.complex64)
+    elif dtype == "i16":
+        cube = rng.integers(-32768, 32768, (nf, nrx, nc, ns, 2)).astype(np.int16)
+    else:
+        cube = rng.uniform(-1, 1, (nf, nrx, nc, ns, 2)).astype(np.float16)
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, N_RX=nrx, in_dtype=dtype, cfar="none", max_frames=nf) as core:
+        got = run_range_ct(core, cube, nf)
+    ref = O.range_ct(to_complex(cube, dtype))
+    for f in range(nf):
+        for rx in range(nrx):
+            assert rel_err(got[f, rx], ref[f, rx]) <= MAP_TOL
+
+
+def test_window_on_gpu_matches_rom(gpu):
+    """Impulse at sample n0 -> |X[r]| = w[n0] for every r, so the GPU's window can be read
+    back and held to tb_window_multiplier.vhd:182-240 (DC endpoint/centre, zero, symmetry)."""
+    ns, nc = 64, 64
+    cube = np.zeros((1, 1, nc, ns), np.complex64)
+    for c in range(ns if ns <= nc else nc):
+        cube[0, 0, c, c % ns] = 1.0
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="none") as core:
+        spec = run_range_ct(core, cube, 1)[0, 0]       # [range][chirp]
+    w = np.abs(spec).mean(axis=0)                       # chirp c carries w[c]
+    np.testing.assert_allclose(w, O.window_f32(ns), rtol=1e-6, atol=1e-7)
+    dc = 16000 * w
+    assert dc[0] <= 3000 and dc[-1] <= 3000 and dc[ns // 2] >= 10000
+    assert np.all(np.abs(w - w[::-1]) <= 1e-6)
+
+
+@pytest.mark.parametrize("case", ["c2_os1d", "c2_os2d", "c3_nci", "ref_core_i16", "small_32"])
+def test_process_parity(gpu, case):
+    """Full path (map + detections) vs the oracle."""
+    cfgs = {
+        "c2_os1d": dict(ns=1024, nc=256, nrx=1, dtype="f32", cfar="os1d", nf=2, recipe="two_targets"),
+        "c2_os2d": dict(ns=1024, nc=256, nrx=1, dtype="f32", cfar="os2d", nf=2, recipe="random_target"),
+        "c3_nci": dict(ns=4096, nc=512, nrx=4, dtype="f32", cfar="os2d", nf=1, recipe="two_targets"),
+        "ref_core_i16": dict(ns=1024, nc=128, nrx=1, dtype="i16", cfar="os2d", nf=2, recipe="random_target"),
+        "small_32": dict(ns=128, nc=32, nrx=1, dtype="f32", cfar="os1d", nf=3, recipe="two_targets"),
+    }
+    k = cfgs[case]
+    cube = synth.frames(k["nf"], k["ns"], k["nc"], k["nrx"], k["recipe"], dtype=k["dtype"])
+    with RadarCore(N_RANGE=k["ns"], N_DOPPLER=k["nc"], N_RX=k["nrx"], in_dtype=k["dtype"],
+                   cfar=k["cfar"], max_frames=k["nf"]) as core:
+        out = core.process(cube)
+        # stage exactness: the GPU CFAR on its own map == oracle CFAR on that map
+        exact = run_cfar_stage(core, out.rd_map)
+    cf = O.Cfar1D() if k["cfar"] == "os1d" else O.Cfar2D()
+    ref_mag = np.stack([O.process(to_complex(cube[f], k["dtype"]), None)["mag"] for f in range(k["nf"])])
+    check_map(out.rd_map, ref_mag)
+    want = oracle_dets(out.rd_map, cf)
+    np.testing.assert_array_equal(out.dets, want)        # fused path, bit-exact
+    np.testing.assert_array_equal(exact, want)           # stand-alone fmcw_cfar
+    # vs the fp64 end-to-end oracle: differences only at near-threshold cells
+    ref_dets = oracle_dets(ref_mag.astype(np.float32), cf)
+    a = set(zip(out.dets["frame"].tolist(), out.dets["range"].tolist(), out.dets["doppler"].tolist()))
+    b = set(zip(ref_dets["frame"].tolist(), ref_dets["range"].tolist(), ref_dets["doppler"].tolist()))
+    for (f, r, d) in a ^ b:
+        det, thr = (O.cfar_os1d if k["cfar"] == "os1d" else O.cfar_os2d)(ref_mag[f].astype(np.float32), cf)
+        assert abs(ref_mag[f, r, d] - thr[r, d]) <= 1e-4 * max(thr[r, d], 1e-30), (f, r, d)
+    if k["recipe"] == "two_targets":
+        ns = k["ns"]
+        hit = {(int(r), int(d)) for r, d in zip(out.dets["range"], out.dets["doppler"])}
+        assert (round(100 * ns / 1024), 5) in hit
+
+
+def test_golden_chirp_config1(gpu):
+    """BASELINE config 1: data/golden_input_chirp.txt framed as 128 x 256."""
+    z = np.load(GOLDEN / "golden_chirp_c1.npz")
+    with RadarCore(N_RANGE=256, N_DOPPLER=128, cfar="os1d") as core:
+        out = core.process(z["cube"])
+    check_map(out.rd_map[:, :, :], z["mag"][None])
+    r, d = np.unravel_index(np.argmax(out.rd_map[0]), out.rd_map[0].shape)
+    assert (r, d) == (73, 0)
+    np.testing.assert_array_equal(out.dets, oracle_dets(out.rd_map, O.Cfar1D()))
+
+
+def test_tb_cfar2d_map_gpu(gpu):
+    """rtl/src/tb_os_cfar_2d.vhd map (64 x 32) with its generics, through fmcw_cfar:
+    identical to the committed oracle fixture; both targets found (tb asserts >= 2)."""
+    z = np.load(GOLDEN / "tb_cfar2d.npz")
+    rr, gr, rd, gd = z["params"].tolist()
+    with RadarCore(N_RANGE=64, N_DOPPLER=32, CFAR_REF_R=rd, CFAR_GUARD_R=gd, CFAR_REF_D=rr,
+                   CFAR_GUARD_D=gr, cfar="os2d") as core:
+        got = run_cfar_stage(core, z["map"].astype(np.float32)[None])
+    np.testing.assert_array_equal(got, z["dets"])
+    pos = set(zip(got["range"].tolist(), got["doppler"].tolist()))
+    assert (30, 16) in pos and (50, 8) in pos
+
+
+@pytest.mark.parametrize("override", [0, 2, 5])
+def test_cfar2d_brackets_and_override(gpu, override):
+    """Scale bracket logic (os_cfar_2d.vhd:191-199) incl. scale_override, on a map with
+    clutter (scale_max) and quiet (scale_min) regions; bit-exact vs oracle."""
+    rng = np.random.default_rng(5 + override)
+    m = rng.rayleigh(10.0, (2, 128, 64)).astype(np.float32)
+    m[:, 30:40, 10:20] = rng.rayleigh(200.0, (2, 10, 10))
+    m[:, 80:100, 30:50] = 0.05
+    m[0, 50, 7] = 400.0
+    m[1, 90, 40] = 3.0
+    with RadarCore(N_RANGE=128, N_DOPPLER=64, cfar="os2d", cfar_scale_ovr=override, max_frames=2) as core:
+        got = run_cfar_stage(core, m)
+    np.testing.assert_array_equal(got, oracle_dets(m, O.Cfar2D(scale_override=override)))
+
+
+def test_cfar1d_custom_params(gpu):
+    rng = np.random.default_rng(9)
+    m = rng.rayleigh(1.0, (3, 64, 128)).astype(np.float32)
+    m[1, 10, 100] = 30
+    with RadarCore(N_RANGE=64, N_DOPPLER=128, cfar="os1d", cfar1d=(6, 1, 9, 3.0), max_frames=3) as core:
+        got = run_cfar_stage(core, m)
+    np.testing.assert_array_equal(got, oracle_dets(m, O.Cfar1D(ref=6, guard=1, rank=9, alpha=3.0)))
+
+
+def test_zero_and_saturated_frames(gpu):
+    ns, nc = 256, 64
+    cube = np.zeros((2, 1, nc, ns, 2), np.int16)
+    cube[1] = 32767
+    cube[1, ..., 1] = -32768
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, in_dtype="i16", cfar="os2d", max_frames=2) as core:
+        out = core.process(cube)
+    assert np.all(out.rd_map[0] == 0)
+    assert out.n_dets == len(oracle_dets(out.rd_map, O.Cfar2D()))
+    ref = O.process(to_complex(cube[1], "i16"), None)["mag"]
+    check_map(out.rd_map[1:], ref[None])
+
+
+def test_detection_cap_and_errors(gpu):
+    ns, nc = 256, 64
+    rng = np.random.default_rng(3)
+    m = rng.rayleigh(1.0, (1, ns, nc)).astype(np.float32)
+    m[0, ::8, ::4] = 100.0                        # many detections
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os1d") as core:
+        full = run_cfar_stage(core, m)
+        assert len(full) > 100
+        cube = synth.frames(1, ns, nc)
+        out = core.process(cube, det_cap=None)
+        # explicit small cap -> FMCW_EDETCAP with the required count
+        from fmcw import FmcwError
+        from fmcw import _lib as L
+        if out.n_dets > 1:
+            with pytest.raises(FmcwError) as e:
+                core.process(cube, det_cap=1)
+            assert e.value.code == L.FMCW_EDETCAP
+        with pytest.raises(ValueError):
+            core.process(np.zeros(5, np.complex64))   # not a whole frame
+        with pytest.raises(FmcwError):
+            core.process(synth.frames(2, ns, nc))     # more than max_frames
+
+
+def test_batch_invariance_and_determinism(gpu):
+    """Full BASELINE config 2 size, 64 frames: every frame of a batch equals that frame
+    processed alone (bit-exact), two runs are bit-identical, and scaling the input by 2
+    scales the map by exactly 2 with identical detections (fp32 power-of-two scaling)."""
+    ns, nc, nf = 1024, 256, 64
+    uniq = synth.frames(8, ns, nc, recipe="random_target", seed=77)
+    cube = np.concatenate([uniq] * (nf // 8))
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os1d", max_frames=nf, chunk_frames=16) as core:
+        a = core.process(cube)
+        b = core.process(cube)
+        c = core.process((cube * 2).astype(np.complex64))
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os1d", max_frames=1) as single:
+        s3 = single.process(cube[3:4])
+    np.testing.assert_array_equal(a.rd_map, b.rd_map)
+    np.testing.assert_array_equal(a.dets, b.dets)
+    np.testing.assert_array_equal(a.rd_map[3], s3.rd_map[0])
+    np.testing.assert_array_equal(a.rd_map[11], a.rd_map[3])     # same input frame
+    np.testing.assert_array_equal(c.rd_map, 2 * a.rd_map)
+    np.testing.assert_array_equal(c.dets[["frame", "range", "doppler"]], a.dets[["frame", "range", "doppler"]])
+    f3 = a.dets[a.dets["frame"] == 3]
+    np.testing.assert_array_equal(f3[["range", "doppler", "mag", "threshold"]],
+                                  s3.dets[["range", "doppler", "mag", "threshold"]])
+
+
+def test_db_map(gpu):
+    ns, nc = 512, 64
+    cube = synth.frames(1, ns, nc)
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os1d", map_kind="db") as core:
+        out = core.process(cube)
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os1d") as core:
+        lin = core.process(cube)
+    np.testing.assert_allclose(out.rd_map, O.log_mag(lin.rd_map.astype(np.float64)), atol=2e-4)
+    np.testing.assert_array_equal(out.dets, lin.dets)        # CFAR runs on the linear map

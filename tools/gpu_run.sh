@@ -1,0 +1,32 @@
+#!/usr/bin/env bash
+# Run GPU steps on the gpurun box, each under its own time limit; stop at the first step that
+# crashes, aborts or times out (exit codes other than 0 / 1), continue past plain test failures.
+# usage: tools/gpu_run.sh <step>...   steps: smoke tests bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p "$OUT"
+run() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -n 25 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP: $name exited $rc"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    smoke) run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    tests_all) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    bench) run bench 600 python bench.py --steps 10 --warmup 3 ;;
+    prof) run rocprof_stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "=== all done"
