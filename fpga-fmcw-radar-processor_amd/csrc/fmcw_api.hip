@@ -66,6 +66,7 @@ struct fmcw_handle {
   uint32_t* wg_base = nullptr;
   uint32_t* wg_count = nullptr;
   uint32_t* wg_off = nullptr;
+  uint32_t* block_sum = nullptr;  // ceil(n_wg_max / 1024) scan blocks
   uint32_t* n_dets_tmp = nullptr;
   size_t n_wg_max = 0;
   // grid sizes
@@ -337,15 +338,17 @@ int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipS
 int launch_det_finish(fmcw_handle* h, size_t n_frames, fmcw_det* dets, size_t det_cap,
                       uint32_t* n_dets_dev, hipStream_t s) {
   const int n = (int)(n_frames * tiles_per_frame(h));
+  const int nb = (n + 1023) / 1024;
   ProfScope ps(h, FMCW_K_COMPACT, s);
-  hipLaunchKernelGGL(k_det_scan, dim3(1), dim3(1024), 0, s, h->wg_count, h->wg_off, n, n_dets_dev);
+  hipLaunchKernelGGL(k_det_scan_blocks, dim3(nb), dim3(1024), 0, s, h->wg_count, h->wg_off, n, h->block_sum);
+  hipLaunchKernelGGL(k_det_scan_top, dim3(1), dim3(1024), 0, s, h->block_sum, nb, n_dets_dev);
   int rc = check_launch("k_det_scan");
   if (rc) return rc;
   if (dets && det_cap) {
     // entries past the handle's scratch capacity are never stored: clip to it as well
     const uint32_t cap = (uint32_t)std::min<size_t>(det_cap, h->det_scratch_cap);
     hipLaunchKernelGGL(k_det_copy, dim3((n + 255) / 256), dim3(256), 0, s, h->det_scratch,
-                       h->det_scratch_cap, h->wg_base, h->wg_count, h->wg_off, n, dets, cap);
+                       h->det_scratch_cap, h->wg_base, h->wg_count, h->wg_off, h->block_sum, n, dets, cap);
     rc = check_launch("k_det_copy");
   }
   return rc;
@@ -462,6 +465,7 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   ALLOC(h->wg_base, h->n_wg_max * sizeof(uint32_t));
   ALLOC(h->wg_count, h->n_wg_max * sizeof(uint32_t));
   ALLOC(h->wg_off, h->n_wg_max * sizeof(uint32_t));
+  ALLOC(h->block_sum, ((h->n_wg_max + 1023) / 1024 + 1) * sizeof(uint32_t));
 #undef ALLOC
   {
     std::vector<float> wr = window_table(c.n_range, c.window), wd = window_table(c.n_doppler, c.window);
@@ -490,7 +494,7 @@ int fmcw_destroy(fmcw_handle* h) {
   if (!h) return FMCW_OK;
   hipSetDevice(h->cfg.device_id);
   void* ptrs[] = {h->win_r, h->win_d, h->inter, h->lin_scratch, h->det_scratch, h->counter,
-                  h->n_dets_tmp, h->wg_base, h->wg_count, h->wg_off};
+                  h->n_dets_tmp, h->wg_base, h->wg_count, h->wg_off, h->block_sum};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& pe : h->pending) {

@@ -200,31 +200,76 @@ struct Cfar1DArgs {
 };
 
 // 1-D OS-CFAR along Doppler (circular) over an LDS block of RW magnitude rows (row stride
-// `rs` floats, index pad16(d)), plus ordered emission.  Thread (rr, t) tests cells
-// d = t + P i.  detect <=> #{refs : fl(alpha*ref) >= cut} < n_ref - rank, which is
+// `rs` floats, index pad16(d)), plus ordered emission.  Thread (rr, t) tests the 16
+// consecutive cells d0 = 16 t .. d0 + 15, so emission in thread order is (range, doppler)
+// order.  detect <=> #{refs : fl(alpha*ref) >= cut} < n_ref - rank, which is
 // cut > fl(alpha * sorted(refs)[rank]) (rtl/old/os_cfar.vhd:330-369) without a sort.
-template <int NC, int NT>
+// REF > 0: compile-time geometry (REF refs + GUARD guards per side) with the whole window in
+// registers; REF == 0: runtime geometry read from LDS.
+template <int REF, int GUARD>
+__device__ __forceinline__ float ranked_of(float (&r)[2 * REF], int rank) {
+  // exact k-th smallest of 2*REF registers: bitonic sort (compile-time indices), then a
+  // predicated pick of element `rank` (no runtime register indexing)
+  constexpr int N = 2 * REF;
+  static_assert((N & (N - 1)) == 0, "power-of-two reference count");
+#pragma unroll
+  for (int k = 2; k <= N; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const int l = i ^ j;
+        if (l > i) {
+          const float a = r[i], b = r[l];
+          const bool up = (i & k) == 0;
+          r[i] = up ? fminf(a, b) : fmaxf(a, b);
+          r[l] = up ? fmaxf(a, b) : fminf(a, b);
+        }
+      }
+  float out = r[0];
+#pragma unroll
+  for (int i = 1; i < N; ++i) out = (i == rank) ? r[i] : out;
+  return out;
+}
+
+template <int NC, int NT, int REF, int GUARD>
 __device__ __forceinline__ void cfar1d_emit(const float* mags, int rs, int rr, int t, int r0, int frame,
                                             int wg, const Cfar1DArgs& cf, const DetSink& sink,
                                             int* s_scan) {
-  constexpr int P = NC / 16;
-  constexpr int CELLS = NC / P;  // 16
+  constexpr int CELLS = 16;
   const float* mrow = mags + rr * rs;
+  const int d0 = t * CELLS;
   const int nref = 2 * cf.ref;
   const int need = nref - cf.rank;
   uint32_t bits = 0;
+  if constexpr (REF > 0) {
+    constexpr int H = REF + GUARD, W = CELLS + 2 * H;
+    float v[W];
 #pragma unroll
-  for (int i = 0; i < CELLS; ++i) {
-    const int d = t + P * i;
-    const float cut = mrow[pad16(d)];
-    int cnt = 0;
-    for (int j = 1; j <= cf.ref; ++j) {
-      const float a = mrow[pad16((d - cf.guard - j) & (NC - 1))];
-      const float b = mrow[pad16((d + cf.guard + j) & (NC - 1))];
-      cnt += (cf.alpha * a >= cut) ? 1 : 0;
-      cnt += (cf.alpha * b >= cut) ? 1 : 0;
+    for (int k = 0; k < W; ++k) v[k] = mrow[pad16((d0 - H + k) & (NC - 1))];
+#pragma unroll
+    for (int i = 0; i < CELLS; ++i) {
+      const float cut = v[i + H];
+      int cnt = 0;
+#pragma unroll
+      for (int j = 0; j < REF; ++j) {
+        cnt += (cf.alpha * v[i + j] >= cut) ? 1 : 0;
+        cnt += (cf.alpha * v[i + REF + 2 * GUARD + 1 + j] >= cut) ? 1 : 0;
+      }
+      bits |= (cnt < need ? 1u : 0u) << i;
     }
-    if (cnt < need) bits |= 1u << i;
+  } else {
+#pragma unroll
+    for (int i = 0; i < CELLS; ++i) {
+      const int d = d0 + i;
+      const float cut = mrow[pad16(d)];
+      int cnt = 0;
+      for (int j = 1; j <= cf.ref; ++j) {
+        cnt += (cf.alpha * mrow[pad16((d - cf.guard - j) & (NC - 1))] >= cut) ? 1 : 0;
+        cnt += (cf.alpha * mrow[pad16((d + cf.guard + j) & (NC - 1))] >= cut) ? 1 : 0;
+      }
+      bits |= (cnt < need ? 1u : 0u) << i;
+    }
   }
   int total;
   const int excl = block_excl_scan<NT>(__popc(bits), s_scan, total);
@@ -239,23 +284,30 @@ __device__ __forceinline__ void cfar1d_emit(const float* mags, int rs, int rr, i
   if (!bits) return;
   const uint32_t base = (uint32_t)s_scan[NT / 64 + 1];
   int o = excl;
-  for (int i = 0; i < CELLS; ++i) {
-    if (!((bits >> i) & 1u)) continue;
-    const int d = t + P * i;
-    const float cut = mrow[pad16(d)];
-    // exact ranked reference cell: the value with #less <= rank < #less_or_equal
+  for (uint32_t m = bits; m; m &= m - 1, ++o) {   // detections only (rare): exact ranked ref
+    const int d = d0 + __builtin_ctz(m);
     float ranked = 0.f;
-    for (int j = 0; j < nref; ++j) {
-      const int oj = j < cf.ref ? -(cf.guard + 1 + j) : (cf.guard + 1 + j - cf.ref);
-      const float vj = mrow[pad16((d + oj) & (NC - 1))];
-      int lt = 0, le = 0;
-      for (int i2 = 0; i2 < nref; ++i2) {
-        const int o2 = i2 < cf.ref ? -(cf.guard + 1 + i2) : (cf.guard + 1 + i2 - cf.ref);
-        const float v2 = mrow[pad16((d + o2) & (NC - 1))];
-        lt += v2 < vj;
-        le += v2 <= vj;
+    if constexpr (REF > 0) {
+      float r[2 * REF];
+#pragma unroll
+      for (int j = 0; j < REF; ++j) {
+        r[j] = mrow[pad16((d - GUARD - 1 - j) & (NC - 1))];
+        r[REF + j] = mrow[pad16((d + GUARD + 1 + j) & (NC - 1))];
       }
-      if (lt <= cf.rank && cf.rank < le) ranked = vj;
+      ranked = ranked_of<REF, GUARD>(r, cf.rank);
+    } else {
+      for (int j = 0; j < nref; ++j) {
+        const int oj = j < cf.ref ? -(cf.guard + 1 + j) : (cf.guard + 1 + j - cf.ref);
+        const float vj = mrow[pad16((d + oj) & (NC - 1))];
+        int lt = 0, le = 0;
+        for (int i2 = 0; i2 < nref; ++i2) {
+          const int o2 = i2 < cf.ref ? -(cf.guard + 1 + i2) : (cf.guard + 1 + i2 - cf.ref);
+          const float v2 = mrow[pad16((d + o2) & (NC - 1))];
+          lt += v2 < vj;
+          le += v2 <= vj;
+        }
+        if (lt <= cf.rank && cf.rank < le) ranked = vj;
+      }
     }
     const uint32_t slot = base + (uint32_t)o;
     if (slot < sink.cap) {
@@ -263,12 +315,22 @@ __device__ __forceinline__ void cfar1d_emit(const float* mags, int rs, int rr, i
       dd.frame = (uint32_t)frame;
       dd.range = (uint16_t)(r0 + rr);
       dd.doppler = (uint16_t)d;
-      dd.mag = cut;
+      dd.mag = mrow[pad16(d)];
       dd.threshold = cf.alpha * ranked;
       sink.scratch[slot] = dd;
     }
-    ++o;
   }
+}
+
+// Dispatch on the compile-time fast path (the reference geometry REF 8 / GUARD 2).
+template <int NC, int NT>
+__device__ __forceinline__ void cfar1d_dispatch(const float* mags, int rs, int rr, int t, int r0, int frame,
+                                                int wg, const Cfar1DArgs& cf, const DetSink& sink,
+                                                int* s_scan) {
+  if (cf.ref == 8 && cf.guard == 2 && 2 * (8 + 2) + 16 <= NC + 16)
+    cfar1d_emit<NC, NT, 8, 2>(mags, rs, rr, t, r0, frame, wg, cf, sink, s_scan);
+  else
+    cfar1d_emit<NC, NT, 0, 0>(mags, rs, rr, t, r0, frame, wg, cf, sink, s_scan);
 }
 
 // Stand-alone 1-D OS-CFAR over a caller-supplied [frame][range][doppler] map (fmcw_cfar).
@@ -282,9 +344,9 @@ k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int til
   constexpr int REGM = padded(NC);
   __shared__ __attribute__((aligned(16))) float mags[RW * REGM];
   __shared__ int s_scan[NT / 64 + 2];
-  const int tid = threadIdx.x, rr = tid / P, t = tid % P;
   const int tiles_per_frame = ns / RW;
   for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const int tid = opaque(threadIdx.x), rr = tid / P, t = tid % P;
     const int f = tile / tiles_per_frame;
     const int r0 = (tile - f * tiles_per_frame) * RW;
     const float* src = map + ((size_t)f * ns + r0) * NC;
@@ -294,7 +356,7 @@ k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int til
       mags[rl * REGM + pad16(d)] = src[e];
     }
     __syncthreads();
-    cfar1d_emit<NC, NT>(mags, REGM, rr, t, r0, frame0 + f, tile0 + tile, cf, sink, s_scan);
+    cfar1d_dispatch<NC, NT>(mags, REGM, rr, t, r0, frame0 + f, tile0 + tile, cf, sink, s_scan);
   }
 }
 
@@ -419,7 +481,7 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
       }
     }
     if (cf.enabled)
-      cfar1d_emit<NC, NT>(mags, REGM, rr, t, r0, frame0 + f, tile0 + tile, cf, sink, s_scan);
+      cfar1d_dispatch<NC, NT>(mags, REGM, rr, t, r0, frame0 + f, tile0 + tile, cf, sink, s_scan);
     __syncthreads();  // mags / lds reused by the next tile
   }
 }
@@ -619,32 +681,47 @@ constexpr size_t cfar2d_smem_bytes(int hr) {
 // Detection ordering: exclusive scan over per-workgroup counts (in workgroup = (frame,
 // range) order), then copy each workgroup's run to its final place.
 // --------------------------------------------------------------------------------------
+// level 1: per 1024-entry block, exclusive scan -> wg_off (block-local) + block sums
 __global__ void __launch_bounds__(1024)
-k_det_scan(const uint32_t* __restrict__ wg_count, uint32_t* __restrict__ wg_off, int n,
-           uint32_t* __restrict__ n_dets) {
+k_det_scan_blocks(const uint32_t* __restrict__ wg_count, uint32_t* __restrict__ wg_off, int n,
+                  uint32_t* __restrict__ block_sum) {
   __shared__ int s_wave[1024 / 64 + 2];
-  const int tid = threadIdx.x;
-  const int per = (n + 1023) / 1024;
-  const int b = tid * per;
-  const int e = min(b + per, n);
+  const int i = blockIdx.x * 1024 + threadIdx.x;
+  const int v = i < n ? (int)wg_count[i] : 0;
+  int total;
+  const int e = block_excl_scan<1024>(v, s_wave, total);
+  if (i < n) wg_off[i] = (uint32_t)e;
+  if (threadIdx.x == 0) block_sum[blockIdx.x] = (uint32_t)total;
+}
+
+// level 2: one workgroup scans the block sums in place (-> block offsets) and the total
+__global__ void __launch_bounds__(1024)
+k_det_scan_top(uint32_t* __restrict__ block_sum, int nb, uint32_t* __restrict__ n_dets) {
+  __shared__ int s_wave[1024 / 64 + 2];
+  const int per = (nb + 1023) / 1024;
+  const int b = threadIdx.x * per;
+  const int e = min(b + per, nb);
   uint32_t s = 0;
-  for (int i = b; i < e; ++i) s += wg_count[i];
+  for (int i = b; i < e; ++i) s += block_sum[i];
   int total;
   uint32_t run = (uint32_t)block_excl_scan<1024>((int)s, s_wave, total);
   for (int i = b; i < e; ++i) {
-    wg_off[i] = run;
-    run += wg_count[i];
+    const uint32_t c = block_sum[i];
+    block_sum[i] = run;
+    run += c;
   }
-  if (tid == 0) *n_dets = (uint32_t)total;
+  if (threadIdx.x == 0) *n_dets = (uint32_t)total;
 }
 
 __global__ void k_det_copy(const fmcw_det* __restrict__ scratch, uint32_t scratch_cap,
                            const uint32_t* __restrict__ wg_base, const uint32_t* __restrict__ wg_count,
-                           const uint32_t* __restrict__ wg_off, int n, fmcw_det* __restrict__ out,
-                           uint32_t cap) {
+                           const uint32_t* __restrict__ wg_off, const uint32_t* __restrict__ block_off,
+                           int n, fmcw_det* __restrict__ out, uint32_t cap) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint32_t c = wg_count[i], b = wg_base[i], o = wg_off[i];
+  const uint32_t c = wg_count[i];
+  if (!c) return;
+  const uint32_t b = wg_base[i], o = block_off[i >> 10] + wg_off[i];
   for (uint32_t k = 0; k < c; ++k)
     if (b + k < scratch_cap && o + k < cap) out[o + k] = scratch[b + k];
 }

@@ -46,7 +46,6 @@ def gather_detections(dets, n_dets, frame_offset: int, group=None):
         return rec[:0].clone(), counts
     pad = torch.zeros((m, 4), dtype=torch.int32, device=dev)
     pad[:n] = mine
-    out = torch.empty((world * m, 4), dtype=torch.int32, device=dev)
-    dist.all_gather_into_tensor(out, pad, group=group)
-    parts = [out[r * m: r * m + counts[r]] for r in range(world)]
-    return torch.cat(parts), counts
+    outs = [torch.empty((m, 4), dtype=torch.int32, device=dev) for _ in range(world)]
+    dist.all_gather(outs, pad, group=group)        # one ring all-gather (RCCL / gloo)
+    return torch.cat([outs[r][:counts[r]] for r in range(world)]), counts

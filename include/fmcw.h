@@ -17,7 +17,8 @@
  *   fmcw_det               det_tdata[16:0] / det_range_bin[9:0] / det_doppler_bin[6:0]
  *                          (radar_core.vhd:31-35) + frame index + threshold (dbg_threshold,
  *                          rtl/src/os_cfar_2d.vhd:34, :219)
- *   FMCW_S_SATURATION etc. status_overflow (radar_core.vhd:447-456)
+ *   FMCW_EDETCAP          the sticky status_overflow flag (radar_core.vhd:447-456): the fp32
+ *                          datapath cannot saturate, the detection list can overflow
  *   fmcw_range_ct          window_multiplier -> xfft_range -> corner_turner (:267-327),
  *                          corner-turned spectrum as the CT emits it (corner_turner.vhd:80)
  *   fmcw_magnitude         magnitude_calc (rtl/src/magnitude_calc.vhd:45-88)
@@ -120,6 +121,11 @@ typedef enum {
   FMCW_K_COUNT = 4
 } fmcw_kernel_id;
 
+/* Only the functions below are exported from libfmcw.so (built -fvisibility=hidden). */
+#if defined(__GNUC__)
+#pragma GCC visibility push(default)
+#endif
+
 const char* fmcw_version(void);
 int fmcw_abi_version(void);
 const char* fmcw_last_error(void);
@@ -160,6 +166,10 @@ int fmcw_device_alloc(size_t bytes, void** ptr, int device_id);
 int fmcw_device_free(void* ptr);
 int fmcw_memcpy(void* dst, const void* src, size_t bytes, int kind /*0 H2D,1 D2H,2 D2D*/);
 int fmcw_device_count(int* n);
+
+#if defined(__GNUC__)
+#pragma GCC visibility pop
+#endif
 
 #ifdef __cplusplus
 }

@@ -232,7 +232,7 @@ def test_detection_cap_and_errors(gpu):
     ns, nc = 256, 64
     rng = np.random.default_rng(3)
     m = rng.rayleigh(1.0, (1, ns, nc)).astype(np.float32)
-    m[0, ::8, ::4] = 100.0                        # many detections
+    m[0, ::2, ::16] = 100.0                       # many isolated spikes (>10 cells apart)
     with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os1d") as core:
         full = run_cfar_stage(core, m)
         assert len(full) > 100
