@@ -203,30 +203,26 @@ __device__ __forceinline__ void stockham_from(float2* buf, int t) {
   }
 }
 
-// Radix of the last pass and the L it runs at, for the "last pass to registers" variant.
-template <int N> struct LastPass {
-  static constexpr int rem_after(int L) { return N / L; }
-  static constexpr int find_L() {
-    int L = 8;
+// Radix of the last pass when the passes start at sub-transform size L0.
+template <int N, int L0> struct FinalRadix {
+  static constexpr int calc() {
+    int L = L0;
     while (N / L > 16) L *= 16;
-    return L;
+    return N / L;
   }
-  static constexpr int Lp = find_L();
-  static constexpr int R = N / Lp;
+  static constexpr int R = calc();
+  static constexpr int G = 16 / R;
 };
 
-// All passes after pass 0 except the last, which stays in registers: on return
-// out[g][m] holds X[d] for d = (t + P g) + m * (N / R) with R = LastPass<N>::R.
+// All passes from sub-transform size L except the last, which stays in registers: on
+// return out[g][m] holds X[d] for d = (t + P g) + m * (N / R), R = FinalRadix<N, L>::R.
 template <int N, int L, int P, bool WG_SYNC>
-__device__ __forceinline__ void stockham_to_regs(float2* buf, int t, float2 (*out)[LastPass<N>::R]) {
-  constexpr int LP = LastPass<N>::Lp;
-  if constexpr (L < LP) {
-    constexpr int REM = N / L;
-    constexpr int R = REM >= 16 ? 16 : REM;
-    stockham_pass<N, R, L, P, WG_SYNC>(buf, t);
-    stockham_to_regs<N, L * R, P, WG_SYNC>(buf, t, out);
+__device__ __forceinline__ void stockham_to_regs(float2* buf, int t, float2 (*out)[FinalRadix<N, L>::R]) {
+  if constexpr (N / L > 16) {
+    stockham_pass<N, 16, L, P, WG_SYNC>(buf, t);
+    stockham_to_regs<N, L * 16, P, WG_SYNC>(buf, t, out);
   } else {
-    constexpr int R = LastPass<N>::R;
+    constexpr int R = N / L;
     constexpr int G = N / R / P;
 #pragma unroll
     for (int g = 0; g < G; ++g) {

@@ -115,9 +115,13 @@ struct DopplerInfo {
   DopplerFn fn;
   int RW, NT;
 };
-DopplerInfo doppler_info(uint32_t nc) {
+template <int N>
+DopplerFn doppler_fn(int mti) {
+  return mti == FMCW_MTI_2PULSE ? k_doppler<N, 2> : mti == FMCW_MTI_3PULSE ? k_doppler<N, 3> : k_doppler<N, 0>;
+}
+DopplerInfo doppler_info(uint32_t nc, int mti = FMCW_MTI_OFF) {
   switch (nc) {
-#define D_(N) case N: return {k_doppler<N>, DopplerGeom<N>::RW, DopplerGeom<N>::NT};
+#define D_(N) case N: return {doppler_fn<N>(mti), DopplerGeom<N>::RW, DopplerGeom<N>::NT};
     D_(32) D_(64) D_(128) D_(256) D_(512) D_(1024)
 #undef D_
   }
@@ -203,6 +207,8 @@ int validate(const fmcw_config& c) {
     return fail(FMCW_EINVAL, "mag_mode AMBM is defined for n_rx == 1 only");
   if (c.map_kind != FMCW_MAP_LINEAR && c.map_kind != FMCW_MAP_DB)
     return fail(FMCW_EINVAL, "map_kind=%d unknown", c.map_kind);
+  if (c.mti_mode != FMCW_MTI_OFF && c.mti_mode != FMCW_MTI_2PULSE && c.mti_mode != FMCW_MTI_3PULSE)
+    return fail(FMCW_EINVAL, "mti_mode=%d unknown (0 off, 2 or 3 pulse)", c.mti_mode);
   if (range_info(c.n_range, c.in_dtype).T > (int)c.n_doppler)
     return fail(FMCW_EINVAL, "n_doppler=%u smaller than the range kernel's chirp group", c.n_doppler);
   if (c.max_frames < 1) return fail(FMCW_EINVAL, "max_frames must be >= 1");
@@ -475,7 +481,7 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
       return cleanup(fail(FMCW_EHIP, "window upload failed"));
   }
   occupancy_grid(ri.fn, ri.NT, 0, h->n_cu, &h->grid_range);
-  const DopplerInfo di = doppler_info(c.n_doppler);
+  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode);
   occupancy_grid(di.fn, di.NT, 0, h->n_cu, &h->grid_doppler);
   if (c.cfar_kind == FMCW_CFAR_OS2D) {
     const Cfar2DArgs a = cfar2_args(c);
@@ -516,7 +522,7 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
     return fail(FMCW_EINVAL, "n_dets_dev is required when a CFAR is configured");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const RangeInfo ri = range_info(c.n_range, c.in_dtype);
-  const DopplerInfo di = doppler_info(c.n_doppler);
+  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode);
   const size_t frame_px = (size_t)c.n_range * c.n_doppler;
   const size_t in_frame_bytes = cube_bytes(c, 1);
   const Cfar1DArgs cf1 = cfar1_args(c);

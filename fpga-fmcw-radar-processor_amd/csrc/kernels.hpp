@@ -363,6 +363,11 @@ k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int til
 // --------------------------------------------------------------------------------------
 // K2: Doppler window + FFT + magnitude (+NCI over rx) + map + 1-D OS-CFAR.
 // One workgroup = RW range bins x all NC chirps of one frame; grid-stride over tiles.
+// Thread (rr, t) of P = NC/16 owns range row r0 + rr's transform, which lives inside one
+// wave, so its LDS row is wave-private and the FFT needs no workgroup barrier.  Pass 1
+// (radix 16, no twiddles) reads its 16 points c = t + P m straight from the tiled spectrum
+// (8-byte loads, contiguous across the wave's rows and lanes), windowed on the way in; the
+// last pass stays in registers and feeds |X|^2 (summed over rx: NCI) directly.
 // --------------------------------------------------------------------------------------
 template <int NC> struct DopplerGeom {
   static constexpr int P = NC / 16;
@@ -370,11 +375,11 @@ template <int NC> struct DopplerGeom {
   static constexpr int NT = RW * P;
   static constexpr int REGD = padded(NC) + 4;           // complex per range row in LDS
   static constexpr int REGM = padded(NC);               // floats per range row (magnitudes)
-  static constexpr int LR = LastPass<NC>::R;
+  static constexpr int LR = FinalRadix<NC, 16>::R;      // last pass radix (after pass 1)
   static constexpr int LG = 16 / LR;
 };
 
-template <int NC>
+template <int NC, int MTI>
 __global__ void __launch_bounds__(DopplerGeom<NC>::NT)
 k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int ns, int nrx,
           int lgT, int lgRB, int n_tiles, int frame0, int tile0, float* __restrict__ lin_map,
@@ -382,23 +387,30 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
   using Gm = DopplerGeom<NC>;
   constexpr int P = Gm::P, RW = Gm::RW, NT = Gm::NT, REGD = Gm::REGD, REGM = Gm::REGM;
   constexpr int LR = Gm::LR, LG = Gm::LG;
-  constexpr int PIECES = RW * NC / 2 / NT;  // 8 pieces of (r, c..c+1) per thread
+  static_assert(P <= 64, "a Doppler transform must fit one wave");
   __shared__ __attribute__((aligned(16))) float2 lds[RW * REGD];
   __shared__ __attribute__((aligned(16))) float mags[RW * REGM];
   __shared__ int s_scan[NT / 64 + 2];
 
   const int rr = threadIdx.x / P;
+  const int t0 = threadIdx.x % P;
   const int tiles_per_frame = ns / RW;
   const int T = 1 << lgT;
-  const int lgRWT = __builtin_ctz(RW) + lgT;
   const int lgncb = __builtin_ctz(NC) - lgT;
+  // window for this thread's chirps c = t + P m (loop-invariant, kept in registers)
+  float wv[16];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) wv[m] = win_d[t0 + P * m];
 
   for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-    const int tid = opaque(threadIdx.x);
-    const int t = tid % P;
+    const int t = opaque(t0);
     float2* buf = lds + rr * REGD;
     const int f = tile / tiles_per_frame;
     const int r0 = (tile - f * tiles_per_frame) * RW;
+    const int r = r0 + rr;
+    // element (r, c) of the tiled spectrum: ((rb*NCB + c/T)*RB + r%RB)*T + c%T
+    const uint32_t rbase = (uint32_t)(r >> lgRB) << lgncb;
+    const uint32_t rin = (uint32_t)(r & ((1 << lgRB) - 1));
     float acc[LG][LR];
 #pragma unroll
     for (int g = 0; g < LG; ++g)
@@ -407,48 +419,48 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
 
     for (int rx = 0; rx < nrx; ++rx) {
       const float2* src = inter + ((size_t)f * nrx + rx) * (size_t)ns * NC;
-      // stage RW x NC complex from the tiled corner-turn layout, windowed on the way in
-      float4 x[PIECES];
+      auto at = [&](uint32_t c) -> float2 {
+        const uint32_t off = ((((rbase + (c >> lgT)) << lgRB) + rin) << lgT) | (c & (uint32_t)(T - 1));
+        return src[off];
+      };
+      float2 v[16];
 #pragma unroll
-      for (int i = 0; i < PIECES; ++i) {
-        const int e = 2 * (tid + NT * i);
-        const int cbi = e >> lgRWT;
-        const int wi = e & ((1 << lgRWT) - 1);
-        const int r = r0 + (wi >> lgT);
-        const int ci = wi & (T - 1);
-        const size_t off = ((((size_t)(r >> lgRB) << lgncb) + cbi) << lgRB | (r & ((1 << lgRB) - 1))) << lgT | ci;
-        x[i] = *reinterpret_cast<const float4*>(src + off);
+      for (int m = 0; m < 16; ++m) {
+        const int c = t + P * m;
+        float2 x = at((uint32_t)c);
+        if constexpr (MTI >= 2) {  // MTI canceller along slow time, zero history (doppler_notch.vhd:72-102)
+          const float2 x1 = c >= 1 ? at((uint32_t)(c - 1)) : make_float2(0.f, 0.f);
+          if constexpr (MTI == 2) {
+            x = csub(x, x1);
+          } else {
+            const float2 x2 = c >= 2 ? at((uint32_t)(c - 2)) : make_float2(0.f, 0.f);
+            x = cadd(csub(x, cscale(x1, 2.f)), x2);
+          }
+        }
+        v[m] = cscale(x, wv[m]);
       }
-      __syncthreads();  // lds free (previous rx / tile done)
+      Dft<16>::run(v);                       // pass 1: L = 1, no twiddles
+      {
+        float2* d = buf + pad16(16 * t);     // y[16 t + m]
 #pragma unroll
-      for (int i = 0; i < PIECES; ++i) {
-        const int e = 2 * (tid + NT * i);
-        const int cbi = e >> lgRWT;
-        const int wi = e & ((1 << lgRWT) - 1);
-        const int rl = wi >> lgT;
-        const int c = (cbi << lgT) | (wi & (T - 1));
-        const float2 wv = *reinterpret_cast<const float2*>(win_d + c);
-        float2* d = lds + rl * REGD + pad16(c);  // c even: c, c+1 share a 16-block
-        d[0] = make_float2(x[i].x * wv.x, x[i].y * wv.x);
-        d[1] = make_float2(x[i].z * wv.y, x[i].w * wv.y);
+        for (int m = 0; m < 16; ++m) d[m] = v[m];
       }
-      __syncthreads();
-      stockham_from<NC, 1, P, false>(buf, t);  // NC <= 1024: one transform per wave
+      pass_sync<false>();
+      float2 X[LG][LR];
+      stockham_to_regs<NC, 16, P, false>(buf, t, X);
 #pragma unroll
-      for (int g = 0; g < LG; ++g) {
-        const float2* s0 = buf + pad16(t + P * g);
+      for (int g = 0; g < LG; ++g)
 #pragma unroll
         for (int m = 0; m < LR; ++m) {
-          const float2 X = s0[padoff(m * (NC / LR))];
           if (mag_mode == FMCW_MAG_AMBM) {
-            const float ai = fabsf(X.x), aq = fabsf(X.y);
+            const float ai = fabsf(X[g][m].x), aq = fabsf(X[g][m].y);
             const float mx = fmaxf(ai, aq), mn = fminf(ai, aq);
             acc[g][m] = mx + floorf(mn * 0.25f) + floorf(mn * 0.125f);
           } else {
-            acc[g][m] += X.x * X.x + X.y * X.y;
+            acc[g][m] += X[g][m].x * X[g][m].x + X[g][m].y * X[g][m].y;
           }
         }
-      }
+      pass_sync<false>();  // next rx overwrites this wave's row
     }
     // magnitudes -> LDS (for the map store and the CFAR neighbourhood)
     float* mrow = mags + rr * REGM;
@@ -465,6 +477,7 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
     {
       constexpr int Q = RW * NC / 4 / NT;
       const size_t mbase = ((size_t)f * ns + r0) * NC;
+      const int tid = rr * P + t;
 #pragma unroll
       for (int i = 0; i < Q; ++i) {
         const int e = 4 * (tid + NT * i);

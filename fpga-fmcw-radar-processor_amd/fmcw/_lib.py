@@ -22,6 +22,7 @@ WIN_NONE, WIN_HAMMING = 0, 1
 MAG_ABS, MAG_AMBM = 0, 1
 MAP_LINEAR, MAP_DB = 1, 2
 CFAR_NONE, CFAR_OS1D, CFAR_OS2D = 0, 1, 2
+MTI_OFF, MTI_2PULSE, MTI_3PULSE = 0, 2, 3
 K_RANGE, K_DOPPLER, K_CFAR2D, K_COMPACT, K_COUNT = 0, 1, 2, 3, 4
 KERNEL_NAMES = ("k_range", "k_doppler", "k_cfar", "k_compact")
 
@@ -33,7 +34,7 @@ class FmcwConfig(C.Structure):
     _fields_ = [
         ("n_range", C.c_uint32), ("n_doppler", C.c_uint32), ("n_rx", C.c_uint32),
         ("in_dtype", C.c_int32), ("window", C.c_int32), ("mag_mode", C.c_int32),
-        ("map_kind", C.c_int32), ("cfar_kind", C.c_int32),
+        ("map_kind", C.c_int32), ("cfar_kind", C.c_int32), ("mti_mode", C.c_int32),
         ("cfar1d_ref", C.c_uint32), ("cfar1d_guard", C.c_uint32), ("cfar1d_rank", C.c_uint32),
         ("cfar1d_alpha", C.c_float),
         ("cfar2d_ref_range", C.c_uint32), ("cfar2d_guard_range", C.c_uint32),

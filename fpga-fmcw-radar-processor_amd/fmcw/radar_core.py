@@ -132,9 +132,15 @@ class RadarCore:
                  cfar_rank_pct: int = 75, cfar_scales=(2, 4, 6),
                  cfar1d=(8, 2, 12, 4.0), in_dtype: str = "f32", window: str = "hamming",
                  magnitude: str = "abs", map_kind: str = "linear", max_frames: int = 1,
-                 chunk_frames: int = 0, device: int = 0):
+                 chunk_frames: int = 0, device: int = 0, mti_bypass: bool = True,
+                 NOTCH_MODE: int = 2):
+        """mti_bypass / NOTCH_MODE mirror radar_core's u_mti (radar_core.vhd:329-338, port
+        :48).  The RTL port defaults to '0' (MTI on); this mirror defaults to bypass because
+        the north-star path and BASELINE configs exclude MTI and tb_radar_core bypasses it
+        (rtl/src/tb_radar_core.vhd:66)."""
         lib = L.load()
         cfg = L.default_config()
+        cfg.mti_mode = L.MTI_OFF if mti_bypass else {2: L.MTI_2PULSE, 3: L.MTI_3PULSE}[NOTCH_MODE]
         cfg.n_range, cfg.n_doppler, cfg.n_rx = N_RANGE, N_DOPPLER, N_RX
         cfg.in_dtype = _IN_DTYPES[in_dtype][0]
         cfg.window = {"hamming": L.WIN_HAMMING, "none": L.WIN_NONE}[window]

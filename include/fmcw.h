@@ -69,6 +69,10 @@ typedef enum { FMCW_MAG_ABS = 0, FMCW_MAG_AMBM = 1 } fmcw_mag_mode;
 /* What fmcw_enqueue writes into rd_map: linear magnitude, or 20*log10(mag + 1). */
 typedef enum { FMCW_MAP_LINEAR = 1, FMCW_MAP_DB = 2 } fmcw_map_kind;
 typedef enum { FMCW_CFAR_NONE = 0, FMCW_CFAR_OS1D = 1, FMCW_CFAR_OS2D = 2 } fmcw_cfar_kind;
+/* MTI / Doppler notch on the corner-turned spectrum, along slow time per range bin, delay
+ * line zeroed at each range bin's first chirp (rtl/src/doppler_notch.vhd:72-102):
+ * 2-pulse y[c] = x[c] - x[c-1];  3-pulse y[c] = x[c] - 2 x[c-1] + x[c-2].  OFF = bypass. */
+typedef enum { FMCW_MTI_OFF = 0, FMCW_MTI_2PULSE = 2, FMCW_MTI_3PULSE = 3 } fmcw_mti_mode;
 
 typedef struct fmcw_config {
   uint32_t n_range;        /* Ns: samples per chirp = range bins (N_RANGE); power of 2, 64..8192 */
@@ -79,6 +83,7 @@ typedef struct fmcw_config {
   int32_t mag_mode;        /* fmcw_mag_mode */
   int32_t map_kind;        /* fmcw_map_kind */
   int32_t cfar_kind;       /* fmcw_cfar_kind */
+  int32_t mti_mode;        /* fmcw_mti_mode (mti_bypass port, radar_core.vhd:48) */
   /* 1-D OS-CFAR along Doppler (circular): rtl/old/os_cfar.vhd generics */
   uint32_t cfar1d_ref;     /* reference cells per side (REF_CELLS, 8) */
   uint32_t cfar1d_guard;   /* guard cells per side (GUARD_CELLS, 2) */

@@ -113,6 +113,38 @@ def range_ct(cube: np.ndarray, window: bool = True) -> np.ndarray:
     return np.swapaxes(np.fft.fft(x, axis=-1), -1, -2)
 
 
+def mti(spec_rc: np.ndarray, mode: int) -> np.ndarray:
+    """MTI / Doppler notch (rtl/src/doppler_notch.vhd:72-102) along slow time (last axis) of
+    the corner-turned spectrum, one delay line per range bin zeroed at its first chirp (the
+    reset on tlast, :99-102).  2-pulse y[c] = x[c] - x[c-1]; 3-pulse x[c] - 2x[c-1] + x[c-2].
+    mode 0 = bypass.  Build spec: complex fp arithmetic, no int16 saturation (:76-93)."""
+    x = np.asarray(spec_rc)
+    if mode == 0:
+        return x
+    x1 = np.zeros_like(x)
+    x1[..., 1:] = x[..., :-1]
+    if mode == 2:
+        return x - x1
+    if mode == 3:
+        x2 = np.zeros_like(x)
+        x2[..., 2:] = x[..., :-2]
+        return x - 2 * x1 + x2
+    raise ValueError(mode)
+
+
+def mti_rtl_int16(i: np.ndarray, q: np.ndarray, mode: int):
+    """RTL-compat MTI on int16 I/Q streams (one range bin's slow-time sequence): the same
+    difference with saturation to [-32768, 32767] (doppler_notch.vhd:76-93)."""
+    def one(x):
+        x = np.asarray(x, np.int64)
+        x1 = np.concatenate([[0], x[:-1]])
+        y = x - x1 if mode == 2 else x - 2 * x1 + np.concatenate([[0, 0], x[:-2]])
+        return np.clip(y, -32768, 32767)
+    if mode == 0:
+        return np.asarray(i, np.int64), np.asarray(q, np.int64)
+    return one(i), one(q)
+
+
 def doppler_fft(spec_rc: np.ndarray, window: bool = True) -> np.ndarray:
     """Doppler window over slow time + forward Nc-point FFT per range bin (radar_core.vhd:340-364).
 
@@ -305,7 +337,7 @@ def detections(det: np.ndarray, mag: np.ndarray, thr: np.ndarray, frame: int = 0
 # ---------------------------------------------------------------------------
 
 
-def process(cube: np.ndarray, cfar=None, window: bool = True):
+def process(cube: np.ndarray, cfar=None, window: bool = True, mti_mode: int = 0):
     """Full hot path for one frame.
 
     cube: [rx, chirp, sample] (or [chirp, sample]) complex.  Returns dict with the
@@ -316,7 +348,7 @@ def process(cube: np.ndarray, cfar=None, window: bool = True):
     c = np.asarray(cube)
     if c.ndim == 2:
         c = c[None]
-    rd = doppler_fft(range_ct(c, window), window)  # [rx, range, doppler]
+    rd = doppler_fft(mti(range_ct(c, window), mti_mode), window)  # [rx, range, doppler]
     mag = magnitude(rd, rx_axis=0)
     mag32 = mag.astype(np.float32)
     if cfar is None:

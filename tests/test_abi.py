@@ -43,7 +43,7 @@ def test_gfx950_code_object_present(lib_built):
 
 def test_struct_layouts():
     assert C.sizeof(L.FmcwDet) == 16
-    assert C.sizeof(L.FmcwConfig) == 24 * 4
+    assert C.sizeof(L.FmcwConfig) == 25 * 4
     assert L.FmcwDet.range.offset == 4 and L.FmcwDet.mag.offset == 8
 
 
@@ -66,6 +66,7 @@ def test_defaults_mirror_radar_core(lib_built):
     ("n_doppler", 16, b"n_doppler"), ("n_rx", 0, b"n_rx"),
     ("in_dtype", 7, b"in_dtype"), ("map_kind", 0, b"map_kind"),
     ("cfar_kind", 9, b"cfar_kind"), ("cfar2d_scale_override", 8, b"scale_override"),
+    ("mti_mode", 1, b"mti_mode"),
     ("cfar2d_ref_doppler", 12, b"2-D CFAR"), ("max_frames", 0, b"max_frames"),
 ])
 def test_create_rejects_bad_config(lib_built, field, value, msg):

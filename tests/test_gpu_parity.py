@@ -131,7 +131,8 @@ def test_window_on_gpu_matches_rom(gpu):
     assert np.all(np.abs(w - w[::-1]) <= 1e-6)
 
 
-@pytest.mark.parametrize("case", ["c2_os1d", "c2_os2d", "c3_nci", "ref_core_i16", "small_32"])
+@pytest.mark.parametrize("case", ["c2_os1d", "c2_os2d", "c3_nci", "ref_core_i16", "small_32",
+                                  "mti2_os2d", "mti3_os1d"])
 def test_process_parity(gpu, case):
     """Full path (map + detections) vs the oracle."""
     cfgs = {
@@ -140,16 +141,22 @@ def test_process_parity(gpu, case):
         "c3_nci": dict(ns=4096, nc=512, nrx=4, dtype="f32", cfar="os2d", nf=1, recipe="two_targets"),
         "ref_core_i16": dict(ns=1024, nc=128, nrx=1, dtype="i16", cfar="os2d", nf=2, recipe="random_target"),
         "small_32": dict(ns=128, nc=32, nrx=1, dtype="f32", cfar="os1d", nf=3, recipe="two_targets"),
+        # MTI (doppler_notch, radar_core.vhd:329-338) enabled: the next row of SURVEY.md 8f
+        "mti2_os2d": dict(ns=1024, nc=128, nrx=1, dtype="i16", cfar="os2d", nf=2, recipe="random_target", mti=2),
+        "mti3_os1d": dict(ns=512, nc=64, nrx=2, dtype="f32", cfar="os1d", nf=2, recipe="two_targets", mti=3),
     }
     k = cfgs[case]
+    mti = k.get("mti", 0)
     cube = synth.frames(k["nf"], k["ns"], k["nc"], k["nrx"], k["recipe"], dtype=k["dtype"])
     with RadarCore(N_RANGE=k["ns"], N_DOPPLER=k["nc"], N_RX=k["nrx"], in_dtype=k["dtype"],
-                   cfar=k["cfar"], max_frames=k["nf"]) as core:
+                   cfar=k["cfar"], max_frames=k["nf"], mti_bypass=(mti == 0),
+                   NOTCH_MODE=mti or 2) as core:
         out = core.process(cube)
         # stage exactness: the GPU CFAR on its own map == oracle CFAR on that map
         exact = run_cfar_stage(core, out.rd_map)
     cf = O.Cfar1D() if k["cfar"] == "os1d" else O.Cfar2D()
-    ref_mag = np.stack([O.process(to_complex(cube[f], k["dtype"]), None)["mag"] for f in range(k["nf"])])
+    ref_mag = np.stack([O.process(to_complex(cube[f], k["dtype"]), None, mti_mode=mti)["mag"]
+                        for f in range(k["nf"])])
     check_map(out.rd_map, ref_mag)
     want = oracle_dets(out.rd_map, cf)
     np.testing.assert_array_equal(out.dets, want)        # fused path, bit-exact

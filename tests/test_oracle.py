@@ -124,6 +124,38 @@ def test_tb_cfar2d_map():
     assert (30, 16) in pos and (50, 8) in pos
 
 
+def test_mti_tb_doppler_notch_checks():
+    """rtl/src/tb_doppler_notch.vhd:95-180 (N_DOPPLER 32, amplitude 10000): 2-pulse nulls DC
+    (only the first sample after the reset survives), passes an f=8 tone (avg |y| >= 1000,
+    :139), bypass passes DC (>= 5000, :156), 3-pulse nulls DC, the delay line resets at each
+    sequence (:99-102).  Checked on the fp restatement and on the int16 RTL-compat form."""
+    n = 32
+    s = np.arange(n)
+
+    def chirp(f):
+        ph = 2 * np.pi * f * s / n
+        return np.rint(10000 * np.cos(ph)), np.rint(10000 * np.sin(ph))
+
+    for mode in (2, 3):
+        i, q = chirp(0.0)
+        y = O.mti((i + 1j * q)[None], mode)[0]
+        assert np.all(np.abs(y[mode - 1 + (mode == 3):]) == 0) and abs(y[0]) == 10000
+        yi, yq = O.mti_rtl_int16(i, q, mode)
+        np.testing.assert_array_equal(yi + 1j * yq, y)
+    i, q = chirp(8.0)
+    y2 = O.mti((i + 1j * q)[None], 2)[0]
+    assert np.mean(np.abs(y2)) >= 1000
+    i, q = chirp(0.0)
+    assert np.mean(np.abs(O.mti((i + 1j * q)[None], 0)[0])) >= 5000
+    # reset: two bursts processed as two range bins give identical outputs
+    two = np.stack([i + 1j * q, i + 1j * q])
+    out = O.mti(two, 2)
+    np.testing.assert_array_equal(out[0], out[1])
+    # saturation exists only in the int16 compat form
+    yi, _ = O.mti_rtl_int16(np.array([32767, -32768]), np.array([0, 0]), 2)
+    assert list(yi) == [32767, -32768]
+
+
 def test_cfar_defaults_match_reference_generics():
     """os_cfar_2d as instantiated (radar_core.vhd:376-382): 11 x 13 window, 128 refs, k=96;
     os_cfar 1-D (radar_core_v3.vhd:373-381): 16 refs, k=12, alpha 4."""
