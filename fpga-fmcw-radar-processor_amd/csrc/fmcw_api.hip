@@ -62,7 +62,9 @@ struct fmcw_handle {
   float* lin_scratch = nullptr;  // chunk * ns * nc (2-D CFAR input when the caller wants no linear map)
   fmcw_det* det_scratch = nullptr;
   uint32_t det_scratch_cap = 0;
-  uint32_t* counter = nullptr;
+  uint32_t slot_cap = 32;  // detections per tile slot (sized in fmcw_create; more -> overflow)
+  uint32_t ovf_base = 0;   // first overflow entry
+  uint32_t* counter = nullptr;  // [0] overflow entries used, [1] dropped
   uint32_t* wg_base = nullptr;
   uint32_t* wg_count = nullptr;
   uint32_t* wg_off = nullptr;
@@ -143,9 +145,15 @@ struct Cfar2Info {
   Cfar2Fn fn;
   int TR;
 };
-Cfar2Info cfar2_info(uint32_t nc) {
+// the reference window (Doppler half extent 6, guard 2: os_cfar_2d as instantiated at
+// radar_core.vhd:376-382) gets the compile-time phase A; any other geometry the generic one
+template <int N>
+Cfar2Fn cfar2_fn(int hd, int gd) {
+  return (hd == 6 && gd == 2) ? k_cfar2d<N, 6, 2> : k_cfar2d<N, 0, 0>;
+}
+Cfar2Info cfar2_info(uint32_t nc, int hd = 0, int gd = 0) {
   switch (nc) {
-#define C_(N) case N: return {k_cfar2d<N>, Cfar2DGeom<N>::TR};
+#define C_(N) case N: return {cfar2_fn<N>(hd, gd), Cfar2DGeom<N>::TR};
     C_(32) C_(64) C_(128) C_(256) C_(512) C_(1024)
 #undef C_
   }
@@ -302,6 +310,8 @@ DetSink make_sink(fmcw_handle* h) {
   DetSink s;
   s.scratch = h->det_scratch;
   s.cap = h->det_scratch_cap;
+  s.slot_cap = h->slot_cap;
+  s.ovf_base = h->ovf_base;
   s.counter = h->counter;
   s.wg_base = h->wg_base;
   s.wg_count = h->wg_count;
@@ -323,12 +333,13 @@ int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipS
   const DetSink sink = make_sink(h);
   const int tile0 = (int)(frame0 * tiles_per_frame(h));
   if (c.cfar_kind == FMCW_CFAR_OS2D) {
-    const Cfar2Info ci = cfar2_info(c.n_doppler);
+    const Cfar2DArgs a = cfar2_args(c);
+    const Cfar2Info ci = cfar2_info(c.n_doppler, a.hd, a.gd);
     const int n_tiles = nf * (int)tiles_per_frame(h);
     const int grid = std::min(n_tiles, h->grid_cfar);
     ProfScope ps(h, FMCW_K_CFAR2D, s);
     hipLaunchKernelGGL(ci.fn, dim3(grid), dim3(256), h->cfar2d_smem, s, map_chunk, (int)c.n_range,
-                       n_tiles, frame0, tile0, cfar2_args(c), sink);
+                       n_tiles, frame0, tile0, a, sink);
     return check_launch("k_cfar2d");
   }
   // 1-D on a caller map (fmcw_cfar); inside fmcw_enqueue the 1-D CFAR is fused into K2
@@ -347,7 +358,8 @@ int launch_det_finish(fmcw_handle* h, size_t n_frames, fmcw_det* dets, size_t de
   const int nb = (n + 1023) / 1024;
   ProfScope ps(h, FMCW_K_COMPACT, s);
   hipLaunchKernelGGL(k_det_scan_blocks, dim3(nb), dim3(1024), 0, s, h->wg_count, h->wg_off, n, h->block_sum);
-  hipLaunchKernelGGL(k_det_scan_top, dim3(1), dim3(1024), 0, s, h->block_sum, nb, n_dets_dev);
+  hipLaunchKernelGGL(k_det_scan_top, dim3(1), dim3(1024), 0, s, h->block_sum, nb, n_dets_dev,
+                     (const uint32_t*)(h->counter + 1));
   int rc = check_launch("k_det_scan");
   if (rc) return rc;
   if (dets && det_cap) {
@@ -464,7 +476,19 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   ALLOC(h->inter, h->chunk * frame_inter);
   if (c.cfar_kind == FMCW_CFAR_OS2D) ALLOC(h->lin_scratch, (size_t)h->chunk * c.n_range * c.n_doppler * sizeof(float));
   h->n_wg_max = (size_t)c.max_frames * tiles_per_frame(h);
-  h->det_scratch_cap = (uint32_t)std::min<size_t>((size_t)c.max_frames * 4096, 64u << 20);
+  {
+    // Each tile owns a slot of 1/16 of its cells (a 6.25 % detection density, far above any
+    // sane false-alarm rate); denser tiles spill into a shared overflow region of a further
+    // 1/64 of all cells.  Detections beyond both are counted as dropped (FMCW_EDETCAP).
+    const size_t cells_frame = (size_t)c.n_range * c.n_doppler;
+    const size_t cells_tile = cells_frame / tiles_per_frame(h);
+    h->slot_cap = (uint32_t)std::max<size_t>(32, cells_tile / 16);
+    const size_t slots = h->n_wg_max * h->slot_cap;
+    const size_t ovf = std::max<size_t>((size_t)c.max_frames * cells_frame / 64, 65536);
+    if (slots + ovf > 0x7fffffffu) return cleanup(fail(FMCW_EINVAL, "max_frames too large for the detection scratch"));
+    h->ovf_base = (uint32_t)slots;
+    h->det_scratch_cap = (uint32_t)(slots + ovf);
+  }
   ALLOC(h->det_scratch, (size_t)h->det_scratch_cap * sizeof(fmcw_det));
   ALLOC(h->counter, 16);
   ALLOC(h->n_dets_tmp, 16);
@@ -528,7 +552,7 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
   const Cfar1DArgs cf1 = cfar1_args(c);
   const DetSink sink = make_sink(h);
   int rc;
-  if (c.cfar_kind != FMCW_CFAR_NONE) HIP_TRY(hipMemsetAsync(h->counter, 0, sizeof(uint32_t), s));
+  if (c.cfar_kind != FMCW_CFAR_NONE) HIP_TRY(hipMemsetAsync(h->counter, 0, 2 * sizeof(uint32_t), s));
 
   for (size_t f0 = 0; f0 < n_frames; f0 += h->chunk) {
     const int nf = (int)std::min<size_t>(h->chunk, n_frames - f0);
@@ -605,10 +629,11 @@ int fmcw_process(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
     release();
     return rc;
   }
-  uint32_t nd = 0;
+  uint32_t ndd[2] = {0, 0};  // found, dropped
+  uint32_t& nd = ndd[0];
   hipError_t e = hipSuccess;
   if (c.cfar_kind != FMCW_CFAR_NONE)
-    e = hipMemcpyAsync(&nd, h->n_dets_tmp, sizeof nd, hipMemcpyDeviceToHost, s);
+    e = hipMemcpyAsync(ndd, h->n_dets_tmp, sizeof ndd, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess && rd_map && d_map != rd_map)
     e = hipMemcpyAsync(rd_map, d_map, map_bytes, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -617,9 +642,9 @@ int fmcw_process(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
   release();
   if (e != hipSuccess) return fail(FMCW_EHIP, "fmcw_process: %s", hipGetErrorString(e));
   if (n_dets) *n_dets = nd;
-  if (c.cfar_kind != FMCW_CFAR_NONE && (nd > det_cap || nd > h->det_scratch_cap))
-    return fail(FMCW_EDETCAP, "%u detections, det_cap %zu (handle limit %u)", nd, det_cap,
-                h->det_scratch_cap);
+  if (c.cfar_kind != FMCW_CFAR_NONE && (nd > det_cap || ndd[1] > 0))
+    return fail(FMCW_EDETCAP, "%u detections, det_cap %zu, %u beyond the handle's scratch", nd, det_cap,
+                ndd[1]);
   return FMCW_OK;
 }
 
@@ -669,7 +694,7 @@ int fmcw_cfar(fmcw_handle* h, const float* map, size_t n_frames, fmcw_det* dets,
   if (c.cfar_kind == FMCW_CFAR_NONE) return fail(FMCW_EINVAL, "handle has cfar_kind NONE");
   if (n_frames < 1 || n_frames > c.max_frames) return fail(FMCW_EINVAL, "n_frames out of range");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  HIP_TRY(hipMemsetAsync(h->counter, 0, sizeof(uint32_t), s));
+  HIP_TRY(hipMemsetAsync(h->counter, 0, 2 * sizeof(uint32_t), s));
   int rc = launch_cfar(h, map, (int)n_frames, 0, s);
   if (rc) return rc;
   return launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, s);

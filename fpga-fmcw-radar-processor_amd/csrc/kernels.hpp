@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(RangeGeom<N>::NT)
 k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* __restrict__ win,
         int nc, int n_groups) {
   using Gm = RangeGeom<N>;
-  constexpr int P = Gm::P, T = Gm::T, NT = Gm::NT, RB = Gm::RB, REG = Gm::REG;
+  constexpr int P = Gm::P, T = Gm::T, RB = Gm::RB, REG = Gm::REG;
   __shared__ __attribute__((aligned(16))) float2 lds[T * REG];
 
   const int tid = threadIdx.x;
@@ -153,17 +153,70 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
 }
 
 // --------------------------------------------------------------------------------------
-// Detection sink shared by the CFAR kernels: per-workgroup atomic reservation in a scratch
-// list + (base, count) table; k_det_scan/k_det_copy then order the list by workgroup id,
-// which is (frame, range) order, so the result is deterministic.
+// Detection sink shared by the CFAR kernels.  Tile `wg` (a workgroup's unit: frame, range
+// rows) writes its detections, in (range, doppler) order, to its own fixed slot
+// scratch[wg * slot_cap ...] -- no atomic, no round trip.  Only a tile with more than
+// slot_cap detections reserves room in the overflow region with one atomic (a single global
+// counter serialises at ~88 returning atomics/us, MI355X_MICROARCH "dequeue", which is why
+// the common path must not touch it).  (wg_base, wg_count) per tile then let
+// k_det_scan_* / k_det_copy order the list by tile id = (frame, range): deterministic.
+// Detections that fit nowhere are counted in counter[1] (reported as FMCW_EDETCAP).
 // --------------------------------------------------------------------------------------
 struct DetSink {
   fmcw_det* scratch;
-  uint32_t cap;
-  uint32_t* counter;
+  uint32_t cap;        // total scratch entries (slots + overflow)
+  uint32_t slot_cap;   // entries per tile slot
+  uint32_t ovf_base;   // first entry of the overflow region
+  uint32_t* counter;   // [0] overflow entries used, [1] dropped detections
   uint32_t* wg_base;
   uint32_t* wg_count;
 };
+
+// Reserve a tile's range in the sink: every thread gets the same base.  `total` is uniform;
+// the overflow branch (rare) needs one broadcast through LDS.
+__device__ __forceinline__ uint32_t det_reserve(const DetSink& sink, int wg, int total, int* s_bcast) {
+  uint32_t base = (uint32_t)wg * sink.slot_cap;
+  if ((uint32_t)total > sink.slot_cap) {
+    if (threadIdx.x == 0) {
+      uint32_t b = sink.ovf_base + atomicAdd(sink.counter, (uint32_t)total);
+      if (b + (uint32_t)total > sink.cap) atomicAdd(sink.counter + 1, b + (uint32_t)total - max(b, sink.cap));
+      *s_bcast = (int)b;
+    }
+    __syncthreads();
+    base = (uint32_t)*s_bcast;
+  }
+  if (threadIdx.x == 0) {
+    sink.wg_base[wg] = base;
+    sink.wg_count[wg] = (uint32_t)total;
+  }
+  return base;
+}
+
+// Exclusive scan of one int per thread over the workgroup (one barrier): wave scans by
+// shuffles, each thread then adds the totals of the earlier waves.  s_wave[NT/64] must not
+// be rewritten before every thread has passed (callers end the tile with a barrier).
+template <int NT>
+__device__ __forceinline__ int block_excl_scan1(int v, int* s_wave, int& total) {
+  constexpr int NW = NT / 64;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) s_wave[wv] = x;
+  __syncthreads();
+  int before = 0, all = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const int w = s_wave[i];
+    before += i < wv ? w : 0;
+    all += w;
+  }
+  total = all;
+  return before + x - v;
+}
 
 template <int NT>
 __device__ __forceinline__ int block_excl_scan(int v, int* s_wave, int& total) {
@@ -208,8 +261,9 @@ struct Cfar1DArgs {
 // registers; REF == 0: runtime geometry read from LDS.
 template <int REF, int GUARD>
 __device__ __forceinline__ float ranked_of(float (&r)[2 * REF], int rank) {
-  // exact k-th smallest of 2*REF registers: bitonic sort (compile-time indices), then a
-  // predicated pick of element `rank` (no runtime register indexing)
+  // exact k-th smallest of 2*REF registers: bitonic sort (compile-time indices), then the
+  // max of the ascending prefix r[0..rank] (a select chain `i == rank ? r[i] : out` is turned
+  // by LLVM into a private-array lookup, i.e. a scratch store + indexed load per detection)
   constexpr int N = 2 * REF;
   static_assert((N & (N - 1)) == 0, "power-of-two reference count");
 #pragma unroll
@@ -228,7 +282,7 @@ __device__ __forceinline__ float ranked_of(float (&r)[2 * REF], int rank) {
       }
   float out = r[0];
 #pragma unroll
-  for (int i = 1; i < N; ++i) out = (i == rank) ? r[i] : out;
+  for (int i = 1; i < N; ++i) out = fmaxf(out, i <= rank ? r[i] : r[0]);
   return out;
 }
 
@@ -272,17 +326,9 @@ __device__ __forceinline__ void cfar1d_emit(const float* mags, int rs, int rr, i
     }
   }
   int total;
-  const int excl = block_excl_scan<NT>(__popc(bits), s_scan, total);
-  if (threadIdx.x == 0) {
-    uint32_t base = 0;
-    if (total > 0) base = atomicAdd(sink.counter, (uint32_t)total);
-    sink.wg_base[wg] = base;
-    sink.wg_count[wg] = (uint32_t)total;
-    s_scan[NT / 64 + 1] = (int)base;
-  }
-  __syncthreads();
+  const int excl = block_excl_scan1<NT>(__popc(bits), s_scan, total);
+  const uint32_t base = det_reserve(sink, wg, total, s_scan + NT / 64 + 1);
   if (!bits) return;
-  const uint32_t base = (uint32_t)s_scan[NT / 64 + 1];
   int o = excl;
   for (uint32_t m = bits; m; m &= m - 1, ++o) {   // detections only (rare): exact ranked ref
     const int d = d0 + __builtin_ctz(m);
@@ -334,12 +380,16 @@ __device__ __forceinline__ void cfar1d_dispatch(const float* mags, int rs, int r
 }
 
 // Stand-alone 1-D OS-CFAR over a caller-supplied [frame][range][doppler] map (fmcw_cfar).
+// range rows per 1-D CFAR / Doppler workgroup: 4096 cells, at most 64 rows (= the smallest
+// n_range, so every frame has at least one whole tile)
+constexpr int rows_per_wg(int nc) { return nc >= 1024 ? 4 : (4096 / nc < 64 ? 4096 / nc : 64); }
+
 template <int NC>
-__global__ void __launch_bounds__((NC >= 1024 ? 4 : 4096 / NC) * (NC / 16))
+__global__ void __launch_bounds__(rows_per_wg(NC) * (NC / 16))
 k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int tile0, Cfar1DArgs cf,
          DetSink sink) {
   constexpr int P = NC / 16;
-  constexpr int RW = NC >= 1024 ? 4 : 4096 / NC;
+  constexpr int RW = rows_per_wg(NC);
   constexpr int NT = RW * P;
   constexpr int REGM = padded(NC);
   __shared__ __attribute__((aligned(16))) float mags[RW * REGM];
@@ -371,7 +421,7 @@ k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int til
 // --------------------------------------------------------------------------------------
 template <int NC> struct DopplerGeom {
   static constexpr int P = NC / 16;
-  static constexpr int RW = NC >= 1024 ? 4 : 256 / P;   // range bins per workgroup
+  static constexpr int RW = rows_per_wg(NC);   // range bins per workgroup
   static constexpr int NT = RW * P;
   static constexpr int REGD = padded(NC) + 4;           // complex per range row in LDS
   static constexpr int REGM = padded(NC);               // floats per range row (magnitudes)
@@ -500,195 +550,10 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
 }
 
 // --------------------------------------------------------------------------------------
-// K3: 2-D OS-CFAR (rtl/src/os_cfar_2d.vhd:140-217) over the linear magnitude map.
-// One workgroup = TR CUT rows x all NC Doppler cells of one frame (Doppler circular);
-// the tile plus +-hr halo rows sits in LDS.  Wave w owns rows [w*TR/4, (w+1)*TR/4) so its
-// detections come out in (range, doppler) order.
-//
-// Phase A (one lane per cell): count c = #{refs : fl(s_min * ref) >= cut}.  Because
-// fl(s*x) is monotone in s and x, c >= n_ref - k proves cut <= fl(s * ranked) for every
-// admissible scale s >= s_min: the cell cannot detect.  Almost all noise cells stop here.
-// Phase B (whole wave per surviving cell): lanes hold refs l and l+64; mean from the fixed
-// fp32 halving tree (one add + xor-shuffles 32..1, = oracle tree_sum_f32); the scale
-// bracket from ballot counts (ranked > M <=> #{ref > M} >= n_ref - k; ranked < M' <=>
-// #{ref < M'} >= k + 1); detection <=> #{fl(s*ref) >= cut} < n_ref - k; for detections the
-// exact ranked value by a 32-step radix select on order-preserving keys.
+// K3: 2-D OS-CFAR (rtl/src/os_cfar_2d.vhd:140-217) -- see cfar2d.hpp.
 // --------------------------------------------------------------------------------------
-struct Cfar2DArgs {
-  int hr, gr, hd, gd;  // half extents (ref + guard) and guards, range / Doppler
-  int n_ref, rank;
-  float s_min, sc_min, sc_nom, sc_max;
-  int override_;
-};
+#include "cfar2d.hpp"
 
-template <int NC> struct Cfar2DGeom {
-  static constexpr int NT = 256;
-  static constexpr int TR = 4096 / NC;   // CUT rows per workgroup (4096 cells)
-  static constexpr int CW = 4096 / 4;    // cells per wave
-};
-
-__device__ __forceinline__ uint32_t f2key(float f) {
-  const uint32_t u = __float_as_uint(f);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ __forceinline__ float key2f(uint32_t k) {
-  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
-}
-
-template <int NC>
-__global__ void __launch_bounds__(256)
-k_cfar2d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int tile0, Cfar2DArgs a,
-         DetSink sink) {
-  using Gm = Cfar2DGeom<NC>;
-  constexpr int TR = Gm::TR, CW = Gm::CW, NT = Gm::NT;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  // carve: tile [(TR + 2 hr)][NC] | per-wave lists [4][CW] x (u32 cell, f32 thr) | offsets | scan
-  const int rows_in = TR + 2 * a.hr;
-  float* tile = smem;
-  uint2* lists = reinterpret_cast<uint2*>(smem + ((rows_in * NC + 3) & ~3));
-  short2* offs = reinterpret_cast<short2*>(lists + 4 * CW);
-  int* s_scan = reinterpret_cast<int*>(offs + 128);
-
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  // reference-cell offsets in the fixed order (dr outer, dd inner, guard skipped)
-  if (tid == 0) {
-    int n = 0;
-    for (int dr = -a.hr; dr <= a.hr; ++dr)
-      for (int dd = -a.hd; dd <= a.hd; ++dd) {
-        if (abs(dr) <= a.gr && abs(dd) <= a.gd) continue;
-        offs[n++] = make_short2((short)dr, (short)dd);
-      }
-  }
-  const int need = a.n_ref - a.rank;
-  const int tiles_per_frame = (ns + TR - 1) / TR;
-
-  for (int tl = blockIdx.x; tl < n_tiles; tl += gridDim.x) {
-    const int f = tl / tiles_per_frame;
-    const int r0 = (tl - f * tiles_per_frame) * TR;
-    __syncthreads();
-    // load rows r0-hr .. r0+TR+hr-1 (zero outside the map)
-    const float* fm = map + (size_t)f * ns * NC;
-    for (int e = 4 * tid; e < rows_in * NC; e += 4 * NT) {
-      const int rl = e / NC;
-      const int r = r0 - a.hr + rl;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (r >= 0 && r < ns) v = *reinterpret_cast<const float4*>(fm + (size_t)r * NC + (e - rl * NC));
-      *reinterpret_cast<float4*>(tile + e) = v;
-    }
-    __syncthreads();
-
-    // Phase A: survivors, as one 64-bit mask per 64-cell step of this wave's rows
-    constexpr int STEPS = CW / 64;
-    uint64_t surv[STEPS];
-#pragma unroll
-    for (int s = 0; s < STEPS; ++s) {
-      const int cell = wv * CW + s * 64 + lane;
-      const int rl = cell / NC, d = cell - rl * NC;
-      const int r = r0 + rl;
-      bool sv = false;
-      if (r >= a.hr && r < ns - a.hr) {
-        const float* crow = tile + (rl + a.hr) * NC;
-        const float cut = crow[d];
-        int c = 0;
-        for (int dr = -a.hr; dr <= a.hr; ++dr) {
-          const float* row = crow + dr * NC;
-          const bool grow = abs(dr) <= a.gr;
-          for (int dd = -a.hd; dd <= a.hd; ++dd) {
-            if (grow && abs(dd) <= a.gd) continue;
-            c += (a.s_min * row[(d + dd) & (NC - 1)] >= cut) ? 1 : 0;
-          }
-        }
-        sv = c < need;
-      }
-      surv[s] = __ballot(sv);
-    }
-
-    // Phase B: whole-wave evaluation of each survivor, in cell order
-    int ndet = 0;
-    uint2* mylist = lists + wv * CW;
-#pragma unroll
-    for (int s = 0; s < STEPS; ++s) {
-      uint64_t m = surv[s];
-      while (m) {
-        const int l0 = __builtin_ctzll(m);
-        m &= m - 1;
-        const int cell = wv * CW + s * 64 + l0;
-        const int rl = cell / NC, d = cell - rl * NC;
-        const float* crow = tile + (rl + a.hr) * NC;
-        const float cut = crow[d];
-        float va = 0.f, vb = 0.f;
-        const bool oka = lane < a.n_ref, okb = lane + 64 < a.n_ref;
-        if (oka) { const short2 o = offs[lane]; va = crow[o.x * NC + ((d + o.y) & (NC - 1))]; }
-        if (okb) { const short2 o = offs[lane + 64]; vb = crow[o.x * NC + ((d + o.y) & (NC - 1))]; }
-        float sum = va + vb;
-#pragma unroll
-        for (int x = 32; x >= 1; x >>= 1) sum += __shfl_xor(sum, x, 64);
-        const float mean = sum / (float)a.n_ref;
-        float sc;
-        if (a.override_) {
-          sc = (float)a.override_;
-        } else {
-          const float half = mean * 0.5f;
-          const float hi = mean + half;
-          const int n_hi = __popcll(__ballot(oka && va > hi)) + __popcll(__ballot(okb && vb > hi));
-          const int n_lo = __popcll(__ballot(oka && va < half)) + __popcll(__ballot(okb && vb < half));
-          sc = (n_hi >= need) ? a.sc_max : (n_lo >= a.rank + 1) ? a.sc_min : a.sc_nom;
-        }
-        const int n_ge = __popcll(__ballot(oka && sc * va >= cut)) + __popcll(__ballot(okb && sc * vb >= cut));
-        if (n_ge < need) {
-          // exact k-th smallest (k = rank) by radix select on order keys
-          const uint32_t ka = f2key(va), kb = f2key(vb);
-          uint32_t prefix = 0;
-          int k = a.rank;
-          for (int bit = 31; bit >= 0; --bit) {
-            const uint32_t hmask = bit == 31 ? 0u : ~((2u << bit) - 1u);
-            const bool za = oka && ((ka & hmask) == prefix) && !((ka >> bit) & 1u);
-            const bool zb = okb && ((kb & hmask) == prefix) && !((kb >> bit) & 1u);
-            const int c0 = __popcll(__ballot(za)) + __popcll(__ballot(zb));
-            if (k >= c0) { k -= c0; prefix |= 1u << bit; }
-          }
-          const float ranked = key2f(prefix);
-          if (lane == 0) mylist[ndet] = make_uint2((uint32_t)cell, __float_as_uint(sc * ranked));
-          ++ndet;
-        }
-      }
-    }
-    // ordered emission: waves in order, each list in cell order
-    int total;
-    const int excl = block_excl_scan<NT>(lane == 0 ? ndet : 0, s_scan, total);
-    const int wexcl = __shfl(excl, 0, 64);
-    if (tid == 0) {
-      uint32_t base = 0;
-      if (total > 0) base = atomicAdd(sink.counter, (uint32_t)total);
-      sink.wg_base[tile0 + tl] = base;
-      sink.wg_count[tile0 + tl] = (uint32_t)total;
-      s_scan[NT / 64 + 1] = (int)base;
-    }
-    __syncthreads();
-    const uint32_t base = (uint32_t)s_scan[NT / 64 + 1];
-    for (int i = lane; i < ndet; i += 64) {
-      const uint2 rec = mylist[i];
-      const uint32_t slot = base + (uint32_t)(wexcl + i);
-      if (slot < sink.cap) {
-        const int cell = (int)rec.x;
-        const int rl = cell / NC, d = cell - rl * NC;
-        fmcw_det dd;
-        dd.frame = (uint32_t)(frame0 + f);
-        dd.range = (uint16_t)(r0 + rl);
-        dd.doppler = (uint16_t)d;
-        dd.mag = tile[(rl + a.hr) * NC + d];
-        dd.threshold = __uint_as_float(rec.y);
-        sink.scratch[slot] = dd;
-      }
-    }
-  }
-}
-
-template <int NC>
-constexpr size_t cfar2d_smem_bytes(int hr) {
-  return (size_t)(((Cfar2DGeom<NC>::TR + 2 * hr) * NC + 3) & ~3) * 4 + 4 * Cfar2DGeom<NC>::CW * 8 +
-         128 * 4 + 16 * 4;
-}
 
 // --------------------------------------------------------------------------------------
 // Detection ordering: exclusive scan over per-workgroup counts (in workgroup = (frame,
@@ -709,7 +574,8 @@ k_det_scan_blocks(const uint32_t* __restrict__ wg_count, uint32_t* __restrict__ 
 
 // level 2: one workgroup scans the block sums in place (-> block offsets) and the total
 __global__ void __launch_bounds__(1024)
-k_det_scan_top(uint32_t* __restrict__ block_sum, int nb, uint32_t* __restrict__ n_dets) {
+k_det_scan_top(uint32_t* __restrict__ block_sum, int nb, uint32_t* __restrict__ n_dets,
+               const uint32_t* __restrict__ dropped) {
   __shared__ int s_wave[1024 / 64 + 2];
   const int per = (nb + 1023) / 1024;
   const int b = threadIdx.x * per;
@@ -723,7 +589,10 @@ k_det_scan_top(uint32_t* __restrict__ block_sum, int nb, uint32_t* __restrict__ 
     block_sum[i] = run;
     run += c;
   }
-  if (threadIdx.x == 0) *n_dets = (uint32_t)total;
+  if (threadIdx.x == 0) {
+    n_dets[0] = (uint32_t)total;  // every detection found
+    n_dets[1] = *dropped;         // of which not stored (handle scratch exhausted)
+  }
 }
 
 __global__ void k_det_copy(const fmcw_det* __restrict__ scratch, uint32_t scratch_cap,

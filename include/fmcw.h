@@ -144,8 +144,13 @@ int fmcw_destroy(fmcw_handle* h);
 
 /* Full hot path on n_frames frames, device pointers, asynchronous on `stream`
  * (hipStream_t; NULL = default stream).  rd_map may be NULL.  dets may be NULL when
- * cfar_kind == NONE.  *n_dets_dev (device uint32) receives the total detection count
- * (which may exceed det_cap; entries beyond det_cap are dropped). */
+ * cfar_kind == NONE.  n_dets_dev points at TWO device uint32 words:
+ *   n_dets_dev[0] = detections found (may exceed det_cap; entries beyond det_cap are
+ *                   not written),
+ *   n_dets_dev[1] = detections lost because the handle's internal detection scratch
+ *                   overflowed (a tile with more than its slot that also found the shared
+ *                   overflow region full).  Non-zero means the list is incomplete;
+ *                   fmcw_process returns FMCW_EDETCAP in either case. */
 int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_map,
                  fmcw_det* dets, size_t det_cap, uint32_t* n_dets_dev, void* stream);
 

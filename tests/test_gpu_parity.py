@@ -55,8 +55,8 @@ def run_cfar_stage(core, mag, cap=1 << 16):
     dd = DeviceBuffer(cap * 16)
     dn = DeviceBuffer(16)
     core.cfar(dm, nf, dd, cap, dn)
-    n = int(dn.download(np.uint32, (1,))[0])
-    assert n <= cap
+    n, dropped = (int(x) for x in dn.download(np.uint32, (2,)))
+    assert n <= cap and dropped == 0
     return dd.download(DET_DTYPE, (cap,))[:n]
 
 
@@ -132,6 +132,7 @@ def test_window_on_gpu_matches_rom(gpu):
 
 
 @pytest.mark.parametrize("case", ["c2_os1d", "c2_os2d", "c3_nci", "ref_core_i16", "small_32",
+                                  "min_64x32_os1d", "min_64x32_os2d", "nc1024_os1d",
                                   "mti2_os2d", "mti3_os1d"])
 def test_process_parity(gpu, case):
     """Full path (map + detections) vs the oracle."""
@@ -141,6 +142,10 @@ def test_process_parity(gpu, case):
         "c3_nci": dict(ns=4096, nc=512, nrx=4, dtype="f32", cfar="os2d", nf=1, recipe="two_targets"),
         "ref_core_i16": dict(ns=1024, nc=128, nrx=1, dtype="i16", cfar="os2d", nf=2, recipe="random_target"),
         "small_32": dict(ns=128, nc=32, nrx=1, dtype="f32", cfar="os1d", nf=3, recipe="two_targets"),
+        # smallest geometry (one 64-row tile per frame) and the widest Doppler FFT
+        "min_64x32_os1d": dict(ns=64, nc=32, nrx=1, dtype="f32", cfar="os1d", nf=3, recipe="random_target"),
+        "min_64x32_os2d": dict(ns=64, nc=32, nrx=1, dtype="i16", cfar="os2d", nf=2, recipe="random_target"),
+        "nc1024_os1d": dict(ns=256, nc=1024, nrx=1, dtype="f16", cfar="os1d", nf=1, recipe="two_targets"),
         # MTI (doppler_notch, radar_core.vhd:329-338) enabled: the next row of SURVEY.md 8f
         "mti2_os2d": dict(ns=1024, nc=128, nrx=1, dtype="i16", cfar="os2d", nf=2, recipe="random_target", mti=2),
         "mti3_os1d": dict(ns=512, nc=64, nrx=2, dtype="f32", cfar="os1d", nf=2, recipe="two_targets", mti=3),
@@ -256,6 +261,21 @@ def test_detection_cap_and_errors(gpu):
             core.process(np.zeros(5, np.complex64))   # not a whole frame
         with pytest.raises(FmcwError):
             core.process(synth.frames(2, ns, nc))     # more than max_frames
+
+
+def test_dense_tiles_use_overflow_region(gpu):
+    """Tiles with more detections than their slot (1/16 of the tile's cells) spill into the
+    shared overflow region; the list stays complete and in (frame, range, doppler) order."""
+    ns, nc, nf = 256, 64, 2
+    rng = np.random.default_rng(5)
+    m = rng.rayleigh(1.0, (nf, ns, nc)).astype(np.float32)
+    m[0, :64, ::8] = 100.0       # tile 0 of frame 0: 64 rows x 8 spikes = 512 > slot 256
+    m[1, 128:192, 4::8] = 80.0   # a later tile of frame 1
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os1d", max_frames=nf) as core:
+        got = run_cfar_stage(core, m)
+    ref = oracle_dets(m, O.Cfar1D())
+    assert len(ref) > 1000
+    np.testing.assert_array_equal(got, ref)
 
 
 def test_batch_invariance_and_determinism(gpu):

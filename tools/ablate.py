@@ -46,11 +46,16 @@ def main():
         "chunk128": dict(cfar="os1d", map=True, chunk=128, mti=False),
         "chunk1024": dict(cfar="os1d", map=True, chunk=1024, mti=False),
         "mti2": dict(cfar="os1d", map=True, chunk=0, mti=True),
+        # CFAR phase split: impossible scale / alpha -> no survivors, counting pass only
+        "os1d_a": dict(cfar="os1d", map=True, chunk=0, mti=False, cfar1d=(8, 2, 12, 1000.0)),
+        "os2d_a": dict(cfar="os2d", map=True, chunk=0, mti=False, ovr=7),
+        "os2d_nom": dict(cfar="os2d", map=True, chunk=0, mti=False, ovr=4),
     }
     for name in a.variants.split(","):
         v = variants[name]
+        extra = {"cfar1d": v["cfar1d"]} if "cfar1d" in v else {}
         core = RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar=v["cfar"], max_frames=F, chunk_frames=v["chunk"],
-                         mti_bypass=not v["mti"])
+                         mti_bypass=not v["mti"], cfar_scale_ovr=v.get("ovr", 0), **extra)
 
         def step():
             core.enqueue(cube.data_ptr(), F, rd_map.data_ptr() if v["map"] else 0, dets.data_ptr(),
@@ -69,7 +74,8 @@ def main():
             step()
         kt = core.kernel_times()
         core.close()
-        out = {"variant": name, "frames_per_s": round(F / el), "ms_per_step": round(el * 1e3, 3)}
+        out = {"variant": name, "frames_per_s": round(F / el), "ms_per_step": round(el * 1e3, 3),
+               "dets_per_frame": round(int(nd[0].item()) / F, 1)}
         for k, (ms, n) in kt.items():
             if n:
                 out[k + "_us_per_frame"] = round(ms * 1e3 / (F * a.steps), 4)

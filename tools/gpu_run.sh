@@ -26,6 +26,9 @@ for s in "$@"; do
     prof) run rocprof_stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    ablate) run ablate 600 python tools/ablate.py ${ABLATE_ARGS:-} ;;
+    counters) run counters 120 rocprofv3 -L ;;
+    pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_LDS_BANK_CONFLICT -d "$OUT/pmc_sq" -o run --output-format csv -- python3 tools/ablate.py --frames 256 --steps 2 --variants base ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
