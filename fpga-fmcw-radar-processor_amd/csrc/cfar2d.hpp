@@ -61,34 +61,34 @@ __device__ __forceinline__ uint32_t cfar2d_phase_a(const float* tile, int rl, in
   constexpr int RS = Cfar2DGeom<NC>::RS;
   constexpr int W = 16 + 2 * HD;
   const float* crow = tile + (rl + a.hr) * RS;
-  float cut[16];
-  int c[16];
+  uint32_t cb[16], lt[16];   // cut bits; #{fl(s_min * ref) < cut} (lt_bit: no SGPR masks)
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    cut[i] = crow[pad16(d0 + i)];
-    c[i] = 0;
+    cb[i] = __float_as_uint(crow[pad16(d0 + i)]);
+    lt[i] = 0;
   }
   for (int dr = -a.hr; dr <= a.hr; ++dr) {
     const float* row = crow + dr * RS;
-    float sv[W];
+    uint32_t sb[W];
 #pragma unroll
-    for (int k = 0; k < W; ++k) sv[k] = a.s_min * row[pad16((d0 - HD + k) & (NC - 1))];
+    for (int k = 0; k < W; ++k) sb[k] = __float_as_uint(a.s_min * row[pad16((d0 - HD + k) & (NC - 1))]);
     if (dr >= -a.gr && dr <= a.gr) {  // guard row: skip |dd| <= GD (uniform branch)
 #pragma unroll
       for (int i = 0; i < 16; ++i)
 #pragma unroll
         for (int dd = -HD; dd <= HD; ++dd)
-          if (dd < -GD || dd > GD) c[i] += sv[i + HD + dd] >= cut[i] ? 1 : 0;
+          if (dd < -GD || dd > GD) lt[i] += lt_bit(sb[i + HD + dd], cb[i]);
     } else {
 #pragma unroll
       for (int i = 0; i < 16; ++i)
 #pragma unroll
-        for (int dd = -HD; dd <= HD; ++dd) c[i] += sv[i + HD + dd] >= cut[i] ? 1 : 0;
+        for (int dd = -HD; dd <= HD; ++dd) lt[i] += lt_bit(sb[i + HD + dd], cb[i]);
     }
   }
+  // survivor <=> #{fl(s_min * ref) >= cut} < need  <=>  lt > n_ref - need
   uint32_t bits = 0;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) bits |= (c[i] < need ? 1u : 0u) << i;
+  for (int i = 0; i < 16; ++i) bits |= ((int)lt[i] > a.n_ref - need ? 1u : 0u) << i;
   return bits;
 }
 
@@ -101,17 +101,17 @@ __device__ __forceinline__ uint32_t cfar2d_phase_a_generic(const float* tile, in
   uint32_t bits = 0;
   for (int i = 0; i < 16; ++i) {
     const int d = d0 + i;
-    const float cut = crow[pad16(d)];
-    int c = 0;
+    const uint32_t c = __float_as_uint(crow[pad16(d)]);
+    uint32_t lt = 0;
     for (int dr = -a.hr; dr <= a.hr; ++dr) {
       const float* row = crow + dr * RS;
       const bool grow = dr >= -a.gr && dr <= a.gr;
       for (int dd = -a.hd; dd <= a.hd; ++dd) {
         if (grow && dd >= -a.gd && dd <= a.gd) continue;
-        c += (a.s_min * row[pad16((d + dd) & (NC - 1))] >= cut) ? 1 : 0;
+        lt += lt_bit(__float_as_uint(a.s_min * row[pad16((d + dd) & (NC - 1))]), c);
       }
     }
-    bits |= (c < need ? 1u : 0u) << i;
+    bits |= ((int)lt > a.n_ref - need ? 1u : 0u) << i;
   }
   return bits;
 }

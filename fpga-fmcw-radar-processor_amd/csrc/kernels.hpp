@@ -67,7 +67,7 @@ template <int N> struct RangeGeom {
 template <int N, typename LD>
 __global__ void __launch_bounds__(RangeGeom<N>::NT)
 k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* __restrict__ win,
-        int nc, int n_groups) {
+        const float* __restrict__ chirp_w, int nc, int n_groups) {
   using Gm = RangeGeom<N>;
   constexpr int P = Gm::P, T = Gm::T, RB = Gm::RB, REG = Gm::REG;
   __shared__ __attribute__((aligned(16))) float2 lds[T * REG];
@@ -104,6 +104,8 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
     const int cb = g - fr * ncb;
     const int t = opaque(t0);
     float2* buf = lds + q * REG;
+    // Doppler window of this chirp folded in (K2 then skips it; FFT linearity), or 1
+    const float cw = chirp_w ? chirp_w[cb * T + q] : 1.f;
 
     __syncthreads();  // previous group's transposed reads are done with lds
 #pragma unroll
@@ -111,7 +113,7 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
       float2 v[8];
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
-        const float we = e ? w[m].y : w[m].x;
+        const float we = (e ? w[m].y : w[m].x) * cw;
         v[m] = e ? make_float2(a[m].z * we, a[m].w * we) : make_float2(a[m].x * we, a[m].y * we);
       }
       Dft<8>::run(v);
@@ -246,6 +248,11 @@ __device__ __forceinline__ int block_excl_scan(int v, int* s_wave, int& total) {
   return r;
 }
 
+// 1 if x < y, for non-negative finite floats given as bit patterns (their unsigned order is
+// the float order and |xb - yb| < 2^31).  CFAR inputs are magnitudes (>= +0), like the
+// reference's unsigned magnitude stream (magnitude_calc.vhd).  No VCC / SGPR mask involved.
+__device__ __forceinline__ uint32_t lt_bit(uint32_t xb, uint32_t yb) { return (xb - yb) >> 31; }
+
 struct Cfar1DArgs {
   int enabled;
   int ref, guard, rank;
@@ -255,8 +262,10 @@ struct Cfar1DArgs {
 // 1-D OS-CFAR along Doppler (circular) over an LDS block of RW magnitude rows (row stride
 // `rs` floats, index pad16(d)), plus ordered emission.  Thread (rr, t) tests the 16
 // consecutive cells d0 = 16 t .. d0 + 15, so emission in thread order is (range, doppler)
-// order.  detect <=> #{refs : fl(alpha*ref) >= cut} < n_ref - rank, which is
-// cut > fl(alpha * sorted(refs)[rank]) (rtl/old/os_cfar.vhd:330-369) without a sort.
+// order.  detect <=> #{refs : fl(alpha*ref) >= cut} < n_ref - rank  <=>  #{fl(alpha*ref) <
+// cut} > rank, which is cut > fl(alpha * sorted(refs)[rank]) (rtl/old/os_cfar.vhd:330-369)
+// without a sort.  The count is mask-free integer arithmetic (lt_bit) so that hundreds of
+// compares do not become SGPR masks that spill.
 // REF > 0: compile-time geometry (REF refs + GUARD guards per side) with the whole window in
 // registers; REF == 0: runtime geometry read from LDS.
 template <int REF, int GUARD>
@@ -289,79 +298,94 @@ __device__ __forceinline__ float ranked_of(float (&r)[2 * REF], int rank) {
 template <int NC, int NT, int REF, int GUARD>
 __device__ __forceinline__ void cfar1d_emit(const float* mags, int rs, int rr, int t, int r0, int frame,
                                             int wg, const Cfar1DArgs& cf, const DetSink& sink,
-                                            int* s_scan) {
+                                            int* s_scan, uint32_t* list) {
   constexpr int CELLS = 16;
   const float* mrow = mags + rr * rs;
   const int d0 = t * CELLS;
   const int nref = 2 * cf.ref;
-  const int need = nref - cf.rank;
   uint32_t bits = 0;
   if constexpr (REF > 0) {
     constexpr int H = REF + GUARD, W = CELLS + 2 * H;
-    float v[W];
+    // two halves of 8 cells (a 28-value window each) to keep the register peak low
+    constexpr int HC = CELLS / 2, WH = HC + 2 * H;
+    (void)W;
 #pragma unroll
-    for (int k = 0; k < W; ++k) v[k] = mrow[pad16((d0 - H + k) & (NC - 1))];
+    for (int hh = 0; hh < 2; ++hh) {
+      uint32_t cb[HC], sb[WH];   // cut bits, scaled-window bits
 #pragma unroll
-    for (int i = 0; i < CELLS; ++i) {
-      const float cut = v[i + H];
-      int cnt = 0;
-#pragma unroll
-      for (int j = 0; j < REF; ++j) {
-        cnt += (cf.alpha * v[i + j] >= cut) ? 1 : 0;
-        cnt += (cf.alpha * v[i + REF + 2 * GUARD + 1 + j] >= cut) ? 1 : 0;
+      for (int k = 0; k < WH; ++k) {
+        const float x = mrow[pad16((d0 + hh * HC - H + k) & (NC - 1))];
+        sb[k] = __float_as_uint(cf.alpha * x);
+        if (k >= H && k < H + HC) cb[k - H] = __float_as_uint(x);
       }
-      bits |= (cnt < need ? 1u : 0u) << i;
+#pragma unroll
+      for (int i = 0; i < HC; ++i) {
+        uint32_t lt = 0;
+#pragma unroll
+        for (int j = 0; j < REF; ++j)
+          lt += lt_bit(sb[i + j], cb[i]) + lt_bit(sb[i + REF + 2 * GUARD + 1 + j], cb[i]);
+        bits |= ((int)lt > cf.rank ? 1u : 0u) << (hh * HC + i);
+      }
     }
   } else {
 #pragma unroll
     for (int i = 0; i < CELLS; ++i) {
       const int d = d0 + i;
-      const float cut = mrow[pad16(d)];
-      int cnt = 0;
+      const uint32_t c = __float_as_uint(mrow[pad16(d)]);
+      uint32_t lt = 0;
       for (int j = 1; j <= cf.ref; ++j) {
-        cnt += (cf.alpha * mrow[pad16((d - cf.guard - j) & (NC - 1))] >= cut) ? 1 : 0;
-        cnt += (cf.alpha * mrow[pad16((d + cf.guard + j) & (NC - 1))] >= cut) ? 1 : 0;
+        lt += lt_bit(__float_as_uint(cf.alpha * mrow[pad16((d - cf.guard - j) & (NC - 1))]), c);
+        lt += lt_bit(__float_as_uint(cf.alpha * mrow[pad16((d + cf.guard + j) & (NC - 1))]), c);
       }
-      bits |= (cnt < need ? 1u : 0u) << i;
+      bits |= ((int)lt > cf.rank ? 1u : 0u) << i;
     }
   }
   int total;
   const int excl = block_excl_scan1<NT>(__popc(bits), s_scan, total);
   const uint32_t base = det_reserve(sink, wg, total, s_scan + NT / 64 + 1);
-  if (!bits) return;
-  int o = excl;
-  for (uint32_t m = bits; m; m &= m - 1, ++o) {   // detections only (rare): exact ranked ref
-    const int d = d0 + __builtin_ctz(m);
+  if (total == 0) return;  // uniform
+  // Detections cluster (a target lights up consecutive cells of one thread), so the ranked
+  // value is computed one detection per thread over the whole workgroup, from an ordered
+  // list of cells (rr << 16 | d) in `list` (capacity: the tile's cells).
+  {
+    int o = excl;
+    for (uint32_t m = bits; m; m &= m - 1, ++o) list[o] = ((uint32_t)rr << 16) | (uint32_t)(d0 + __builtin_ctz(m));
+  }
+  __syncthreads();
+  for (int i = (int)threadIdx.x; i < total; i += NT) {
+    const uint32_t cell = list[i];
+    const int rl = (int)(cell >> 16), d = (int)(cell & 0xffffu);
+    const float* row = mags + rl * rs;
     float ranked = 0.f;
     if constexpr (REF > 0) {
       float r[2 * REF];
 #pragma unroll
       for (int j = 0; j < REF; ++j) {
-        r[j] = mrow[pad16((d - GUARD - 1 - j) & (NC - 1))];
-        r[REF + j] = mrow[pad16((d + GUARD + 1 + j) & (NC - 1))];
+        r[j] = row[pad16((d - GUARD - 1 - j) & (NC - 1))];
+        r[REF + j] = row[pad16((d + GUARD + 1 + j) & (NC - 1))];
       }
       ranked = ranked_of<REF, GUARD>(r, cf.rank);
     } else {
       for (int j = 0; j < nref; ++j) {
         const int oj = j < cf.ref ? -(cf.guard + 1 + j) : (cf.guard + 1 + j - cf.ref);
-        const float vj = mrow[pad16((d + oj) & (NC - 1))];
+        const float vj = row[pad16((d + oj) & (NC - 1))];
         int lt = 0, le = 0;
         for (int i2 = 0; i2 < nref; ++i2) {
           const int o2 = i2 < cf.ref ? -(cf.guard + 1 + i2) : (cf.guard + 1 + i2 - cf.ref);
-          const float v2 = mrow[pad16((d + o2) & (NC - 1))];
+          const float v2 = row[pad16((d + o2) & (NC - 1))];
           lt += v2 < vj;
           le += v2 <= vj;
         }
         if (lt <= cf.rank && cf.rank < le) ranked = vj;
       }
     }
-    const uint32_t slot = base + (uint32_t)o;
+    const uint32_t slot = base + (uint32_t)i;
     if (slot < sink.cap) {
       fmcw_det dd;
       dd.frame = (uint32_t)frame;
-      dd.range = (uint16_t)(r0 + rr);
+      dd.range = (uint16_t)(r0 + rl);
       dd.doppler = (uint16_t)d;
-      dd.mag = mrow[pad16(d)];
+      dd.mag = row[pad16(d)];
       dd.threshold = cf.alpha * ranked;
       sink.scratch[slot] = dd;
     }
@@ -372,11 +396,11 @@ __device__ __forceinline__ void cfar1d_emit(const float* mags, int rs, int rr, i
 template <int NC, int NT>
 __device__ __forceinline__ void cfar1d_dispatch(const float* mags, int rs, int rr, int t, int r0, int frame,
                                                 int wg, const Cfar1DArgs& cf, const DetSink& sink,
-                                                int* s_scan) {
+                                                int* s_scan, uint32_t* list) {
   if (cf.ref == 8 && cf.guard == 2 && 2 * (8 + 2) + 16 <= NC + 16)
-    cfar1d_emit<NC, NT, 8, 2>(mags, rs, rr, t, r0, frame, wg, cf, sink, s_scan);
+    cfar1d_emit<NC, NT, 8, 2>(mags, rs, rr, t, r0, frame, wg, cf, sink, s_scan, list);
   else
-    cfar1d_emit<NC, NT, 0, 0>(mags, rs, rr, t, r0, frame, wg, cf, sink, s_scan);
+    cfar1d_emit<NC, NT, 0, 0>(mags, rs, rr, t, r0, frame, wg, cf, sink, s_scan, list);
 }
 
 // Stand-alone 1-D OS-CFAR over a caller-supplied [frame][range][doppler] map (fmcw_cfar).
@@ -393,6 +417,7 @@ k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int til
   constexpr int NT = RW * P;
   constexpr int REGM = padded(NC);
   __shared__ __attribute__((aligned(16))) float mags[RW * REGM];
+  __shared__ uint32_t list[RW * NC];
   __shared__ int s_scan[NT / 64 + 2];
   const int tiles_per_frame = ns / RW;
   for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
@@ -406,7 +431,7 @@ k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int til
       mags[rl * REGM + pad16(d)] = src[e];
     }
     __syncthreads();
-    cfar1d_dispatch<NC, NT>(mags, REGM, rr, t, r0, frame0 + f, tile0 + tile, cf, sink, s_scan);
+    cfar1d_dispatch<NC, NT>(mags, REGM, rr, t, r0, frame0 + f, tile0 + tile, cf, sink, s_scan, list);
   }
 }
 
@@ -430,7 +455,7 @@ template <int NC> struct DopplerGeom {
 };
 
 template <int NC, int MTI>
-__global__ void __launch_bounds__(DopplerGeom<NC>::NT)
+__global__ void __launch_bounds__(DopplerGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(MTI == 0 && NC <= 256 ? 3 : 1)))
 k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int ns, int nrx,
           int lgT, int lgRB, int n_tiles, int frame0, int tile0, float* __restrict__ lin_map,
           float* __restrict__ db_map, int mag_mode, Cfar1DArgs cf, DetSink sink) {
@@ -438,6 +463,7 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
   constexpr int P = Gm::P, RW = Gm::RW, NT = Gm::NT, REGD = Gm::REGD, REGM = Gm::REGM;
   constexpr int LR = Gm::LR, LG = Gm::LG;
   static_assert(P <= 64, "a Doppler transform must fit one wave");
+  static_assert(RW * NC * sizeof(uint32_t) <= RW * REGD * sizeof(float2), "detection list fits the FFT rows");
   __shared__ __attribute__((aligned(16))) float2 lds[RW * REGD];
   __shared__ __attribute__((aligned(16))) float mags[RW * REGM];
   __shared__ int s_scan[NT / 64 + 2];
@@ -447,20 +473,47 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
   const int tiles_per_frame = ns / RW;
   const int T = 1 << lgT;
   const int lgncb = __builtin_ctz(NC) - lgT;
-  // window for this thread's chirps c = t + P m (loop-invariant, kept in registers)
-  float wv[16];
+  // Doppler window for this thread's chirps c = t + P m.  MTI off: K1 already applied it
+  // (chirp_w), so no registers are spent on it here.  MTI on: the canceller must see the
+  // unwindowed spectrum (doppler_notch precedes doppler_fft, radar_core.vhd:329-352).
+  float wv[MTI ? 16 : 1];
+  if constexpr (MTI != 0) {
 #pragma unroll
-  for (int m = 0; m < 16; ++m) wv[m] = win_d[t0 + P * m];
+    for (int m = 0; m < 16; ++m) wv[m] = win_d[t0 + P * m];
+  }
+
+  // element (r, c) of the tiled spectrum: ((rb*NCB + c/T)*RB + r%RB)*T + c%T
+  auto row_base = [&](int tile, int& f, int& r0, uint32_t& rbase, uint32_t& rin) {
+    f = tile / tiles_per_frame;
+    r0 = (tile - f * tiles_per_frame) * RW;
+    const int r = r0 + rr;
+    rbase = (uint32_t)(r >> lgRB) << lgncb;
+    rin = (uint32_t)(r & ((1 << lgRB) - 1));
+  };
+  auto off_of = [&](uint32_t rbase, uint32_t rin, uint32_t c) -> uint32_t {
+    return ((((rbase + (c >> lgT)) << lgRB) + rin) << lgT) | (c & (uint32_t)(T - 1));
+  };
+  // MTI off: the next tile's rx-0 samples are prefetched into registers while this tile
+  // finishes its FFT, magnitudes, map store and CFAR (hides the HBM/MALL round trip).
+  constexpr bool PREFETCH = false;   // measured: ~0.1 us/frame, costs 65 VGPRs (occupancy)
+  float2 pre[PREFETCH ? 16 : 1];
+  if constexpr (PREFETCH) {
+    if ((int)blockIdx.x < n_tiles) {
+      int f, r0;
+      uint32_t rbase, rin;
+      row_base(blockIdx.x, f, r0, rbase, rin);
+      const float2* src = inter + (size_t)f * nrx * (size_t)ns * NC;
+#pragma unroll
+      for (int m = 0; m < 16; ++m) pre[m] = src[off_of(rbase, rin, (uint32_t)(t0 + P * m))];
+    }
+  }
 
   for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     const int t = opaque(t0);
     float2* buf = lds + rr * REGD;
-    const int f = tile / tiles_per_frame;
-    const int r0 = (tile - f * tiles_per_frame) * RW;
-    const int r = r0 + rr;
-    // element (r, c) of the tiled spectrum: ((rb*NCB + c/T)*RB + r%RB)*T + c%T
-    const uint32_t rbase = (uint32_t)(r >> lgRB) << lgncb;
-    const uint32_t rin = (uint32_t)(r & ((1 << lgRB) - 1));
+    int f, r0;
+    uint32_t rbase, rin;
+    row_base(tile, f, r0, rbase, rin);
     float acc[LG][LR];
 #pragma unroll
     for (int g = 0; g < LG; ++g)
@@ -469,15 +522,17 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
 
     for (int rx = 0; rx < nrx; ++rx) {
       const float2* src = inter + ((size_t)f * nrx + rx) * (size_t)ns * NC;
-      auto at = [&](uint32_t c) -> float2 {
-        const uint32_t off = ((((rbase + (c >> lgT)) << lgRB) + rin) << lgT) | (c & (uint32_t)(T - 1));
-        return src[off];
-      };
+      auto at = [&](uint32_t c) -> float2 { return src[off_of(rbase, rin, c)]; };
       float2 v[16];
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int c = t + P * m;
-        float2 x = at((uint32_t)c);
+        float2 x;
+        if constexpr (PREFETCH) {
+          x = rx == 0 ? pre[m] : at((uint32_t)c);
+        } else {
+          x = at((uint32_t)c);
+        }
         if constexpr (MTI >= 2) {  // MTI canceller along slow time, zero history (doppler_notch.vhd:72-102)
           const float2 x1 = c >= 1 ? at((uint32_t)(c - 1)) : make_float2(0.f, 0.f);
           if constexpr (MTI == 2) {
@@ -487,13 +542,25 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
             x = cadd(csub(x, cscale(x1, 2.f)), x2);
           }
         }
-        v[m] = cscale(x, wv[m]);
+        if constexpr (MTI != 0) x = cscale(x, wv[m]);
+        v[m] = x;
       }
       Dft<16>::run(v);                       // pass 1: L = 1, no twiddles
       {
         float2* d = buf + pad16(16 * t);     // y[16 t + m]
 #pragma unroll
         for (int m = 0; m < 16; ++m) d[m] = v[m];
+      }
+      if constexpr (PREFETCH) {
+        const int tn = tile + (int)gridDim.x;
+        if (rx == nrx - 1 && tn < n_tiles) {
+          int fn, r0n;
+          uint32_t rbn, rinn;
+          row_base(tn, fn, r0n, rbn, rinn);
+          const float2* srcn = inter + (size_t)fn * nrx * (size_t)ns * NC;
+#pragma unroll
+          for (int m = 0; m < 16; ++m) pre[m] = srcn[off_of(rbn, rinn, (uint32_t)(t + P * m))];
+        }
       }
       pass_sync<false>();
       float2 X[LG][LR];
@@ -544,7 +611,9 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
       }
     }
     if (cf.enabled)
-      cfar1d_dispatch<NC, NT>(mags, REGM, rr, t, r0, frame0 + f, tile0 + tile, cf, sink, s_scan);
+      // the FFT rows are free now: they hold the detection cell list (RW*NC <= 2*RW*REGD)
+      cfar1d_dispatch<NC, NT>(mags, REGM, rr, t, r0, frame0 + f, tile0 + tile, cf, sink, s_scan,
+                              reinterpret_cast<uint32_t*>(lds));
     __syncthreads();  // mags / lds reused by the next tile
   }
 }

@@ -44,6 +44,7 @@ def main():
         "chunk16": dict(cfar="os1d", map=True, chunk=16, mti=False),
         "chunk64": dict(cfar="os1d", map=True, chunk=64, mti=False),
         "chunk128": dict(cfar="os1d", map=True, chunk=128, mti=False),
+        "chunk256": dict(cfar="os1d", map=True, chunk=256, mti=False),
         "chunk1024": dict(cfar="os1d", map=True, chunk=1024, mti=False),
         "mti2": dict(cfar="os1d", map=True, chunk=0, mti=True),
         # CFAR phase split: impossible scale / alpha -> no survivors, counting pass only

@@ -30,18 +30,18 @@ for line in out.splitlines():
 
 
 def short(n):
-    m = re.match(r"_ZN4fmcw\d+(\w+?)(?:ILi(\d+)(?:EN\w*?(Load\w{3}))?)?E", n)
-    if not m:
+    """Demangle the fmcw kernel names to name<args> (c++filt, template args only)."""
+    try:
+        d = subprocess.run(["c++filt", n], capture_output=True, text=True).stdout.strip()
+    except OSError:
         return n
-    s = m.group(1)
-    if m.group(2):
-        s += f"<{m.group(2)}" + (f",{m.group(3)}" if m.group(3) else "") + ">"
-    return s
+    d = d.replace("fmcw::", "").replace("void ", "")
+    return d.split("(", 1)[0].replace(" ", "")
 
 
 flt = sys.argv[1] if len(sys.argv) > 1 else ""
 for r in rows:
     s = short(r["name"])
     if flt in s:
-        print(f"{s:28s} vgpr={r.get('vgpr', '?'):>3} agpr={r.get('agpr', 0):>3} scratch={r.get('scratch', '?'):>4} "
+        print(f"{s:34s} vgpr={r.get('vgpr', '?'):>3} agpr={r.get('agpr', 0):>3} scratch={r.get('scratch', '?'):>4} "
               f"occ={r.get('occ', '?')} lds={r.get('lds', '?')}")
