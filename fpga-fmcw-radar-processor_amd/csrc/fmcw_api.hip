@@ -42,6 +42,9 @@ int fail(int code, const char* fmt, ...) {
 
 bool pow2(uint32_t x) { return x && !(x & (x - 1)); }
 
+constexpr int kWavesPerBlock = 4;  // DopplerGeom<NC>::WPB: wave tiles per K2 / 1-D CFAR workgroup
+static_assert(kWavesPerBlock == DopplerGeom<256>::WPB, "host and kernel tile geometry");
+
 struct PendingEvent {
   int kid;
   hipEvent_t a, b;
@@ -115,7 +118,7 @@ using DopplerFn = void (*)(const float2*, const float*, int, int, int, int, int,
                            float*, int, Cfar1DArgs, DetSink);
 struct DopplerInfo {
   DopplerFn fn;
-  int RW, NT;
+  int WR, NT;  // range rows per wave tile, threads per workgroup (DopplerGeom::WPB tiles)
 };
 template <int N>
 DopplerFn doppler_fn(int mti) {
@@ -123,7 +126,7 @@ DopplerFn doppler_fn(int mti) {
 }
 DopplerInfo doppler_info(uint32_t nc, int mti = FMCW_MTI_OFF) {
   switch (nc) {
-#define D_(N) case N: return {doppler_fn<N>(mti), DopplerGeom<N>::RW, DopplerGeom<N>::NT};
+#define D_(N) case N: return {doppler_fn<N>(mti), DopplerGeom<N>::WR, DopplerGeom<N>::NT};
     D_(32) D_(64) D_(128) D_(256) D_(512) D_(1024)
 #undef D_
   }
@@ -324,7 +327,7 @@ size_t tiles_per_frame(const fmcw_handle* h) {
     const int tr = cfar2_info(c.n_doppler).TR;
     return (c.n_range + tr - 1) / tr;
   }
-  return c.n_range / doppler_info(c.n_doppler).RW;
+  return c.n_range / doppler_info(c.n_doppler).WR;
 }
 
 // The CFAR launcher shared by fmcw_enqueue (map just produced by K2) and fmcw_cfar.
@@ -344,8 +347,8 @@ int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipS
   }
   // 1-D on a caller map (fmcw_cfar); inside fmcw_enqueue the 1-D CFAR is fused into K2
   const DopplerInfo di = doppler_info(c.n_doppler);
-  const int n_tiles = nf * (int)(c.n_range / di.RW);
-  const int grid = std::min(n_tiles, h->grid_doppler);
+  const int n_tiles = nf * (int)(c.n_range / di.WR);
+  const int grid = std::min((n_tiles + kWavesPerBlock - 1) / kWavesPerBlock, h->grid_doppler);
   ProfScope ps(h, FMCW_K_CFAR2D, s);
   hipLaunchKernelGGL(cfar1_fn(c.n_doppler), dim3(grid), dim3(di.NT), 0, s, map_chunk, (int)c.n_range,
                      n_tiles, frame0, tile0, cfar1_args(c), sink);
@@ -479,12 +482,13 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   if (c.cfar_kind == FMCW_CFAR_OS2D) ALLOC(h->lin_scratch, (size_t)h->chunk * c.n_range * c.n_doppler * sizeof(float));
   h->n_wg_max = (size_t)c.max_frames * tiles_per_frame(h);
   {
-    // Each tile owns a slot of 1/16 of its cells (a 6.25 % detection density, far above any
-    // sane false-alarm rate); denser tiles spill into a shared overflow region of a further
-    // 1/64 of all cells.  Detections beyond both are counted as dropped (FMCW_EDETCAP).
+    // Each tile owns a slot of 1/32 of its cells (a 3 % detection density, far above any
+    // sane false-alarm rate; 32 entries for a 1024-cell wave tile); denser tiles spill into
+    // a shared overflow region of a further 1/64 of all cells.  Detections beyond both are
+    // counted as dropped (FMCW_EDETCAP).
     const size_t cells_frame = (size_t)c.n_range * c.n_doppler;
     const size_t cells_tile = cells_frame / tiles_per_frame(h);
-    h->slot_cap = (uint32_t)std::max<size_t>(32, cells_tile / 16);
+    h->slot_cap = (uint32_t)std::max<size_t>(32, cells_tile / 32);
     const size_t slots = h->n_wg_max * h->slot_cap;
     const size_t ovf = std::max<size_t>((size_t)c.max_frames * cells_frame / 64, 65536);
     if (slots + ovf > 0x7fffffffu) return cleanup(fail(FMCW_EINVAL, "max_frames too large for the detection scratch"));
@@ -574,11 +578,12 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
     if (rd_map && c.map_kind == FMCW_MAP_DB) db = rd_map + f0 * frame_px;
     if (c.cfar_kind == FMCW_CFAR_OS2D && !lin) lin = h->lin_scratch;
     {
-      const int n_tiles = nf * (int)(c.n_range / di.RW);
+      const int n_tiles = nf * (int)(c.n_range / di.WR);
+      const int grid = std::min((n_tiles + kWavesPerBlock - 1) / kWavesPerBlock, h->grid_doppler);
       ProfScope ps(h, FMCW_K_DOPPLER, s);
-      hipLaunchKernelGGL(di.fn, dim3(std::min(n_tiles, h->grid_doppler)), dim3(di.NT), 0, s, h->inter,
+      hipLaunchKernelGGL(di.fn, dim3(grid), dim3(di.NT), 0, s, h->inter,
                          h->win_d, (int)c.n_range, (int)c.n_rx, h->lgT, h->lgRB, n_tiles, (int)f0,
-                         (int)(f0 * (c.n_range / di.RW)), lin, db, c.mag_mode, cf1, sink);
+                         (int)(f0 * (c.n_range / di.WR)), lin, db, c.mag_mode, cf1, sink);
       if ((rc = check_launch("k_doppler"))) return rc;
     }
     if (c.cfar_kind == FMCW_CFAR_OS2D) {

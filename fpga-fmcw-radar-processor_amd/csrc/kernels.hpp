@@ -1,7 +1,7 @@
 // kernels.hpp -- HIP kernels of the FMCW hot path for gfx950.
 //
 //  K1 k_range     window + range FFT + corner turn        (radar_core.vhd:267-327)
-//  K2 k_doppler   Doppler window + FFT + |X| / NCI + map + 1-D OS-CFAR
+//  K2 k_doppler   Doppler window + FFT + |X| / NCI + map + 1-D OS-CFAR, one wave per tile
 //                                                        (radar_core.vhd:340-374, os_cfar.vhd)
 //  K3 k_cfar2d    2-D OS-CFAR over the magnitude map       (os_cfar_2d.vhd:83-230)
 //     k_det_scan / k_det_copy   deterministic detection list (radar_core.vhd:396-418)
@@ -9,7 +9,7 @@
 // Intermediate (corner-turned range spectrum) layout in HBM, per (frame, rx):
 //     inter[rb][cb][RB][T]  complex fp32,  rb = r / RB, cb = c / T
 // where T = chirps per K1 workgroup and RB = 128 / T range bins, so K1 writes whole 1 KiB
-// chunks and K2 reads RW x T x 8 B contiguous runs; element (r, c) sits at
+// chunks and K2 reads runs of (rows per wave) x T x 8 B; element (r, c) sits at
 //     ((rb * NCB + cb) * RB + r % RB) * T + c % T.
 // This is the corner turner's [range][chirp] order (corner_turner.vhd:80,
 // rd_addr = range + doppler * N_RANGE) tiled so both sides stream full lines.
@@ -259,13 +259,69 @@ struct Cfar1DArgs {
   float alpha;
 };
 
-// 1-D OS-CFAR along Doppler (circular) over an LDS block of RW magnitude rows (row stride
-// `rs` floats, index pad16(d)), plus ordered emission.  Thread (rr, t) tests the 16
-// consecutive cells d0 = 16 t .. d0 + 15, so emission in thread order is (range, doppler)
-// order.  detect <=> #{refs : fl(alpha*ref) >= cut} < n_ref - rank  <=>  #{fl(alpha*ref) <
-// cut} > rank, which is cut > fl(alpha * sorted(refs)[rank]) (rtl/old/os_cfar.vhd:330-369)
-// without a sort.  The count is mask-free integer arithmetic (lt_bit) so that hundreds of
-// compares do not become SGPR masks that spill.
+// --------------------------------------------------------------------------------------
+// Wave tiles.  K2 and the stand-alone 1-D CFAR work on tiles of WR = 64 / P range rows x all
+// NC Doppler cells of one frame (P = NC/16 lanes per row, 16 cells per lane), ONE WAVEFRONT
+// per tile: a row's Doppler FFT, its magnitudes, its CFAR window and its detection list all
+// live in that wave's private LDS region, so no workgroup barrier is ever needed.  The waves
+// of a workgroup drift apart freely and one wave's HBM loads overlap another's FFT and CFAR
+// arithmetic (a workgroup is only the unit of LDS allocation).  A tile is also the unit of
+// detection ordering (DetSink tile = (frame, range rows)).
+// --------------------------------------------------------------------------------------
+template <int NC> struct DopplerGeom {
+  static constexpr int P = NC / 16;                     // lanes per range row (16 cells each)
+  static constexpr int WR = 64 / P;                     // range rows per wave tile
+  static constexpr int WPB = 4;                         // waves per workgroup (independent)
+  static constexpr int NT = 64 * WPB;
+  static constexpr int REGD = padded(NC) + 4;           // complex per range row (FFT)
+  static constexpr int REGM = padded(NC);               // floats per range row (magnitudes)
+  static constexpr int WREG = WR * REGD;                // complex per wave region
+  static constexpr int LR = FinalRadix<NC, 16>::R;      // last pass radix (after pass 1)
+  static constexpr int LG = 16 / LR;
+  // the magnitudes and then the detection cell list reuse the wave's FFT rows
+  static_assert(WR * REGM + WR * NC <= 2 * WREG, "magnitudes + cell list fit the wave region");
+};
+
+// Wave-level exclusive scan (shuffles only); `total` = the wave's sum, uniform.
+__device__ __forceinline__ int wave_excl_scan(int v, int& total) {
+  const int lane = threadIdx.x & 63;
+  int x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  total = __shfl(x, 63, 64);
+  return x - v;
+}
+
+// det_reserve for a one-wave tile: its slot, or (rare) a range in the overflow region
+// reserved by lane 0 and broadcast by a shuffle.  `total` is wave-uniform.
+__device__ __forceinline__ uint32_t det_reserve_wave(const DetSink& sink, int tile, int total) {
+  const int lane = threadIdx.x & 63;
+  uint32_t base = (uint32_t)tile * sink.slot_cap;
+  if ((uint32_t)total > sink.slot_cap) {
+    uint32_t b = 0;
+    if (lane == 0) {
+      b = sink.ovf_base + atomicAdd(sink.counter, (uint32_t)total);
+      if (b + (uint32_t)total > sink.cap) atomicAdd(sink.counter + 1, b + (uint32_t)total - max(b, sink.cap));
+    }
+    base = (uint32_t)__shfl((int)b, 0, 64);
+  }
+  if (lane == 0) {
+    sink.wg_base[tile] = base;
+    sink.wg_count[tile] = (uint32_t)total;
+  }
+  return base;
+}
+
+// 1-D OS-CFAR along Doppler (circular) over a wave tile's magnitude rows (row stride
+// padded(NC) floats, index pad16(d)), plus ordered emission.  Lane (rr, t) tests the 16
+// consecutive cells d0 = 16 t .. d0 + 15 of row rr, so emission in lane order is (range,
+// doppler) order.  detect <=> #{refs : fl(alpha*ref) >= cut} < n_ref - rank  <=>
+// #{fl(alpha*ref) < cut} > rank, which is cut > fl(alpha * sorted(refs)[rank])
+// (rtl/old/os_cfar.vhd:330-369) without a sort.  The count is mask-free integer arithmetic
+// (lt_bit) so that hundreds of compares do not become SGPR masks that spill.
 // REF > 0: compile-time geometry (REF refs + GUARD guards per side) with the whole window in
 // registers; REF == 0: runtime geometry read from LDS.
 template <int REF, int GUARD>
@@ -295,20 +351,20 @@ __device__ __forceinline__ float ranked_of(float (&r)[2 * REF], int rank) {
   return out;
 }
 
-template <int NC, int NT, int REF, int GUARD>
-__device__ __forceinline__ void cfar1d_emit(const float* mags, int rs, int rr, int t, int r0, int frame,
-                                            int wg, const Cfar1DArgs& cf, const DetSink& sink,
-                                            int* s_scan, uint32_t* list) {
+template <int NC, int REF, int GUARD>
+__device__ __forceinline__ void cfar1d_wave(const float* mags, uint32_t* list, int rr, int t, int r0,
+                                            int frame, int tile, const Cfar1DArgs& cf,
+                                            const DetSink& sink) {
   constexpr int CELLS = 16;
-  const float* mrow = mags + rr * rs;
+  constexpr int RS = padded(NC);
+  const float* mrow = mags + rr * RS;
   const int d0 = t * CELLS;
   const int nref = 2 * cf.ref;
   uint32_t bits = 0;
   if constexpr (REF > 0) {
-    constexpr int H = REF + GUARD, W = CELLS + 2 * H;
+    constexpr int H = REF + GUARD;
     // two halves of 8 cells (a 28-value window each) to keep the register peak low
     constexpr int HC = CELLS / 2, WH = HC + 2 * H;
-    (void)W;
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       uint32_t cb[HC], sb[WH];   // cut bits, scaled-window bits
@@ -341,21 +397,21 @@ __device__ __forceinline__ void cfar1d_emit(const float* mags, int rs, int rr, i
     }
   }
   int total;
-  const int excl = block_excl_scan1<NT>(__popc(bits), s_scan, total);
-  const uint32_t base = det_reserve(sink, wg, total, s_scan + NT / 64 + 1);
+  const int excl = wave_excl_scan(__popc(bits), total);
+  const uint32_t base = det_reserve_wave(sink, tile, total);
   if (total == 0) return;  // uniform
-  // Detections cluster (a target lights up consecutive cells of one thread), so the ranked
-  // value is computed one detection per thread over the whole workgroup, from an ordered
-  // list of cells (rr << 16 | d) in `list` (capacity: the tile's cells).
+  // Detections cluster (a target lights up consecutive cells of one lane), so the ranked
+  // value is computed one detection per lane over the whole wave, from an ordered list of
+  // cells (rr << 16 | d) in `list` (capacity: the tile's cells).
   {
     int o = excl;
     for (uint32_t m = bits; m; m &= m - 1, ++o) list[o] = ((uint32_t)rr << 16) | (uint32_t)(d0 + __builtin_ctz(m));
   }
-  __syncthreads();
-  for (int i = (int)threadIdx.x; i < total; i += NT) {
+  pass_sync<false>();
+  for (int i = (int)(threadIdx.x & 63); i < total; i += 64) {
     const uint32_t cell = list[i];
     const int rl = (int)(cell >> 16), d = (int)(cell & 0xffffu);
-    const float* row = mags + rl * rs;
+    const float* row = mags + rl * RS;
     float ranked = 0.f;
     if constexpr (REF > 0) {
       float r[2 * REF];
@@ -393,127 +449,103 @@ __device__ __forceinline__ void cfar1d_emit(const float* mags, int rs, int rr, i
 }
 
 // Dispatch on the compile-time fast path (the reference geometry REF 8 / GUARD 2).
-template <int NC, int NT>
-__device__ __forceinline__ void cfar1d_dispatch(const float* mags, int rs, int rr, int t, int r0, int frame,
-                                                int wg, const Cfar1DArgs& cf, const DetSink& sink,
-                                                int* s_scan, uint32_t* list) {
-  if (cf.ref == 8 && cf.guard == 2 && 2 * (8 + 2) + 16 <= NC + 16)
-    cfar1d_emit<NC, NT, 8, 2>(mags, rs, rr, t, r0, frame, wg, cf, sink, s_scan, list);
+template <int NC>
+__device__ __forceinline__ void cfar1d_dispatch(const float* mags, uint32_t* list, int rr, int t, int r0,
+                                                int frame, int tile, const Cfar1DArgs& cf,
+                                                const DetSink& sink) {
+  if (cf.ref == 8 && cf.guard == 2)
+    cfar1d_wave<NC, 8, 2>(mags, list, rr, t, r0, frame, tile, cf, sink);
   else
-    cfar1d_emit<NC, NT, 0, 0>(mags, rs, rr, t, r0, frame, wg, cf, sink, s_scan, list);
+    cfar1d_wave<NC, 0, 0>(mags, list, rr, t, r0, frame, tile, cf, sink);
 }
 
-// Stand-alone 1-D OS-CFAR over a caller-supplied [frame][range][doppler] map (fmcw_cfar).
-// range rows per 1-D CFAR / Doppler workgroup: 4096 cells, at most 64 rows (= the smallest
-// n_range, so every frame has at least one whole tile)
-constexpr int rows_per_wg(int nc) { return nc >= 1024 ? 4 : (4096 / nc < 64 ? 4096 / nc : 64); }
-
+// Stand-alone 1-D OS-CFAR over a caller-supplied [frame][range][doppler] map (fmcw_cfar),
+// on the same wave tiles as K2 (so tile ids, and the detection order, are the same).
 template <int NC>
-__global__ void __launch_bounds__(rows_per_wg(NC) * (NC / 16))
+__global__ void __launch_bounds__(DopplerGeom<NC>::NT)
 k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int tile0, Cfar1DArgs cf,
          DetSink sink) {
-  constexpr int P = NC / 16;
-  constexpr int RW = rows_per_wg(NC);
-  constexpr int NT = RW * P;
-  constexpr int REGM = padded(NC);
-  __shared__ __attribute__((aligned(16))) float mags[RW * REGM];
-  __shared__ uint32_t list[RW * NC];
-  __shared__ int s_scan[NT / 64 + 2];
-  const int tiles_per_frame = ns / RW;
-  for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-    const int tid = opaque(threadIdx.x), rr = tid / P, t = tid % P;
+  using Gm = DopplerGeom<NC>;
+  constexpr int P = Gm::P, WR = Gm::WR, WPB = Gm::WPB, REGM = Gm::REGM;
+  __shared__ __attribute__((aligned(16))) float2 lds[WPB * Gm::WREG];
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float* const mags = reinterpret_cast<float*>(lds + wv * Gm::WREG);
+  uint32_t* const list = reinterpret_cast<uint32_t*>(mags + WR * REGM);
+  const int tiles_per_frame = ns / WR;
+  for (int tile = blockIdx.x * WPB + wv; tile < n_tiles; tile += gridDim.x * WPB) {
+    const int lane = opaque(threadIdx.x & 63);
     const int f = tile / tiles_per_frame;
-    const int r0 = (tile - f * tiles_per_frame) * RW;
+    const int r0 = (tile - f * tiles_per_frame) * WR;
     const float* src = map + ((size_t)f * ns + r0) * NC;
-    __syncthreads();
-    for (int e = tid; e < RW * NC; e += NT) {
+#pragma unroll
+    for (int i = 0; i < WR * NC / 4 / 64; ++i) {
+      const int e = 4 * (lane + 64 * i);
       const int rl = e / NC, d = e - rl * NC;
-      mags[rl * REGM + pad16(d)] = src[e];
+      const float4 v = *reinterpret_cast<const float4*>(src + e);
+      float* dst = mags + rl * REGM + pad16(d);  // d % 4 == 0: the 4 floats share a 16-block
+      dst[0] = v.x;
+      dst[1] = v.y;
+      dst[2] = v.z;
+      dst[3] = v.w;
     }
-    __syncthreads();
-    cfar1d_dispatch<NC, NT>(mags, REGM, rr, t, r0, frame0 + f, tile0 + tile, cf, sink, s_scan, list);
+    pass_sync<false>();
+    cfar1d_dispatch<NC>(mags, list, lane / P, lane % P, r0, frame0 + f, tile0 + tile, cf, sink);
+    pass_sync<false>();  // the region is reused by the next tile
   }
 }
 
 // --------------------------------------------------------------------------------------
-// K2: Doppler window + FFT + magnitude (+NCI over rx) + map + 1-D OS-CFAR.
-// One workgroup = RW range bins x all NC chirps of one frame; grid-stride over tiles.
-// Thread (rr, t) of P = NC/16 owns range row r0 + rr's transform, which lives inside one
-// wave, so its LDS row is wave-private and the FFT needs no workgroup barrier.  Pass 1
-// (radix 16, no twiddles) reads its 16 points c = t + P m straight from the tiled spectrum
-// (8-byte loads, contiguous across the wave's rows and lanes), windowed on the way in; the
-// last pass stays in registers and feeds |X|^2 (summed over rx: NCI) directly.
+// K2: Doppler window + FFT + magnitude (+NCI over rx) + map + 1-D OS-CFAR, one wave tile at a
+// time (see "Wave tiles" above).  Lane (rr, t) of P = NC/16 owns range row r0 + rr's
+// transform.  Pass 1 (radix 16, no twiddles) reads its 16 points c = t + P m straight from
+// the tiled spectrum (8-byte loads: two 256-B runs per load instruction across the wave's
+// rows and lanes); the Doppler window was already applied by K1 (MTI off) or is applied here
+// after the canceller (MTI on); the last pass stays in registers and feeds |X|^2 (summed over
+// rx: NCI) directly.
 // --------------------------------------------------------------------------------------
-template <int NC> struct DopplerGeom {
-  static constexpr int P = NC / 16;
-  static constexpr int RW = rows_per_wg(NC);   // range bins per workgroup
-  static constexpr int NT = RW * P;
-  static constexpr int REGD = padded(NC) + 4;           // complex per range row in LDS
-  static constexpr int REGM = padded(NC);               // floats per range row (magnitudes)
-  static constexpr int LR = FinalRadix<NC, 16>::R;      // last pass radix (after pass 1)
-  static constexpr int LG = 16 / LR;
-};
-
 template <int NC, int MTI>
-__global__ void __launch_bounds__(DopplerGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(MTI == 0 && NC <= 256 ? 3 : 1)))
+__global__ void __launch_bounds__(DopplerGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(MTI == 0 && NC <= 256 ? 3 : 2)))
 k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int ns, int nrx,
           int lgT, int lgRB, int n_tiles, int frame0, int tile0, float* __restrict__ lin_map,
           float* __restrict__ db_map, int mag_mode, Cfar1DArgs cf, DetSink sink) {
   using Gm = DopplerGeom<NC>;
-  constexpr int P = Gm::P, RW = Gm::RW, NT = Gm::NT, REGD = Gm::REGD, REGM = Gm::REGM;
+  constexpr int P = Gm::P, WR = Gm::WR, WPB = Gm::WPB, REGD = Gm::REGD, REGM = Gm::REGM;
   constexpr int LR = Gm::LR, LG = Gm::LG;
   static_assert(P <= 64, "a Doppler transform must fit one wave");
-  static_assert(RW * NC * sizeof(uint32_t) <= RW * REGD * sizeof(float2), "detection list fits the FFT rows");
-  __shared__ __attribute__((aligned(16))) float2 lds[RW * REGD];
-  __shared__ __attribute__((aligned(16))) float mags[RW * REGM];
-  __shared__ int s_scan[NT / 64 + 2];
+  __shared__ __attribute__((aligned(16))) float2 lds[WPB * Gm::WREG];
 
-  const int rr = threadIdx.x / P;
-  const int t0 = threadIdx.x % P;
-  const int tiles_per_frame = ns / RW;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane0 = threadIdx.x & 63;
+  const int rr = lane0 / P;
+  const int t0 = lane0 % P;
+  float2* const wreg = lds + wv * Gm::WREG;
+  float* const mags = reinterpret_cast<float*>(wreg);
+  uint32_t* const list = reinterpret_cast<uint32_t*>(mags + WR * REGM);
+  const int tiles_per_frame = ns / WR;
   const int T = 1 << lgT;
   const int lgncb = __builtin_ctz(NC) - lgT;
-  // Doppler window for this thread's chirps c = t + P m.  MTI off: K1 already applied it
+  // Doppler window for this lane's chirps c = t + P m.  MTI off: K1 already applied it
   // (chirp_w), so no registers are spent on it here.  MTI on: the canceller must see the
   // unwindowed spectrum (doppler_notch precedes doppler_fft, radar_core.vhd:329-352).
-  float wv[MTI ? 16 : 1];
+  float wv_d[MTI ? 16 : 1];
   if constexpr (MTI != 0) {
 #pragma unroll
-    for (int m = 0; m < 16; ++m) wv[m] = win_d[t0 + P * m];
+    for (int m = 0; m < 16; ++m) wv_d[m] = win_d[t0 + P * m];
   }
 
   // element (r, c) of the tiled spectrum: ((rb*NCB + c/T)*RB + r%RB)*T + c%T
-  auto row_base = [&](int tile, int& f, int& r0, uint32_t& rbase, uint32_t& rin) {
-    f = tile / tiles_per_frame;
-    r0 = (tile - f * tiles_per_frame) * RW;
-    const int r = r0 + rr;
-    rbase = (uint32_t)(r >> lgRB) << lgncb;
-    rin = (uint32_t)(r & ((1 << lgRB) - 1));
-  };
   auto off_of = [&](uint32_t rbase, uint32_t rin, uint32_t c) -> uint32_t {
     return ((((rbase + (c >> lgT)) << lgRB) + rin) << lgT) | (c & (uint32_t)(T - 1));
   };
-  // MTI off: the next tile's rx-0 samples are prefetched into registers while this tile
-  // finishes its FFT, magnitudes, map store and CFAR (hides the HBM/MALL round trip).
-  constexpr bool PREFETCH = false;   // measured: ~0.1 us/frame, costs 65 VGPRs (occupancy)
-  float2 pre[PREFETCH ? 16 : 1];
-  if constexpr (PREFETCH) {
-    if ((int)blockIdx.x < n_tiles) {
-      int f, r0;
-      uint32_t rbase, rin;
-      row_base(blockIdx.x, f, r0, rbase, rin);
-      const float2* src = inter + (size_t)f * nrx * (size_t)ns * NC;
-#pragma unroll
-      for (int m = 0; m < 16; ++m) pre[m] = src[off_of(rbase, rin, (uint32_t)(t0 + P * m))];
-    }
-  }
 
-  for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+  for (int tile = blockIdx.x * WPB + wv; tile < n_tiles; tile += gridDim.x * WPB) {
     const int t = opaque(t0);
-    float2* buf = lds + rr * REGD;
-    int f, r0;
-    uint32_t rbase, rin;
-    row_base(tile, f, r0, rbase, rin);
+    float2* buf = wreg + rr * REGD;
+    const int f = tile / tiles_per_frame;
+    const int r0 = (tile - f * tiles_per_frame) * WR;
+    const int r = r0 + rr;
+    const uint32_t rbase = (uint32_t)(r >> lgRB) << lgncb;
+    const uint32_t rin = (uint32_t)(r & ((1 << lgRB) - 1));
     float acc[LG][LR];
 #pragma unroll
     for (int g = 0; g < LG; ++g)
@@ -527,12 +559,7 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int c = t + P * m;
-        float2 x;
-        if constexpr (PREFETCH) {
-          x = rx == 0 ? pre[m] : at((uint32_t)c);
-        } else {
-          x = at((uint32_t)c);
-        }
+        float2 x = at((uint32_t)c);
         if constexpr (MTI >= 2) {  // MTI canceller along slow time, zero history (doppler_notch.vhd:72-102)
           const float2 x1 = c >= 1 ? at((uint32_t)(c - 1)) : make_float2(0.f, 0.f);
           if constexpr (MTI == 2) {
@@ -542,7 +569,7 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
             x = cadd(csub(x, cscale(x1, 2.f)), x2);
           }
         }
-        if constexpr (MTI != 0) x = cscale(x, wv[m]);
+        if constexpr (MTI != 0) x = cscale(x, wv_d[m]);
         v[m] = x;
       }
       Dft<16>::run(v);                       // pass 1: L = 1, no twiddles
@@ -551,53 +578,46 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
 #pragma unroll
         for (int m = 0; m < 16; ++m) d[m] = v[m];
       }
-      if constexpr (PREFETCH) {
-        const int tn = tile + (int)gridDim.x;
-        if (rx == nrx - 1 && tn < n_tiles) {
-          int fn, r0n;
-          uint32_t rbn, rinn;
-          row_base(tn, fn, r0n, rbn, rinn);
-          const float2* srcn = inter + (size_t)fn * nrx * (size_t)ns * NC;
-#pragma unroll
-          for (int m = 0; m < 16; ++m) pre[m] = srcn[off_of(rbn, rinn, (uint32_t)(t + P * m))];
-        }
-      }
       pass_sync<false>();
       float2 X[LG][LR];
       stockham_to_regs<NC, 16, P, false>(buf, t, X);
+      if (mag_mode == FMCW_MAG_AMBM) {  // uniform: one branch for the whole block
 #pragma unroll
-      for (int g = 0; g < LG; ++g)
+        for (int g = 0; g < LG; ++g)
 #pragma unroll
-        for (int m = 0; m < LR; ++m) {
-          if (mag_mode == FMCW_MAG_AMBM) {
+          for (int m = 0; m < LR; ++m) {
             const float ai = fabsf(X[g][m].x), aq = fabsf(X[g][m].y);
             const float mx = fmaxf(ai, aq), mn = fminf(ai, aq);
             acc[g][m] = mx + floorf(mn * 0.25f) + floorf(mn * 0.125f);
-          } else {
-            acc[g][m] += X[g][m].x * X[g][m].x + X[g][m].y * X[g][m].y;
           }
-        }
-      pass_sync<false>();  // next rx overwrites this wave's row
+      } else {
+#pragma unroll
+        for (int g = 0; g < LG; ++g)
+#pragma unroll
+          for (int m = 0; m < LR; ++m) acc[g][m] += X[g][m].x * X[g][m].x + X[g][m].y * X[g][m].y;
+      }
+      pass_sync<false>();  // every read of the last pass is issued: the rows may be rewritten
     }
-    // magnitudes -> LDS (for the map store and the CFAR neighbourhood)
+    // magnitudes -> the wave region (over the dead FFT rows), for the map store and the CFAR
+    const bool ambm = mag_mode == FMCW_MAG_AMBM;
     float* mrow = mags + rr * REGM;
 #pragma unroll
     for (int g = 0; g < LG; ++g) {
       float* m0 = mrow + pad16(t + P * g);
 #pragma unroll
       for (int m = 0; m < LR; ++m)
-        m0[padoff(m * (NC / LR))] = (mag_mode == FMCW_MAG_AMBM) ? acc[g][m] : sqrtf(acc[g][m]);
+        m0[padoff(m * (NC / LR))] = ambm ? acc[g][m] : sqrtf(acc[g][m]);
     }
-    __syncthreads();
+    pass_sync<false>();
 
-    // map store: RW*NC floats contiguous at [f][r0][0]
+    // map store: WR*NC = 1024 floats contiguous at [f][r0][0], 16 B per lane
     {
-      constexpr int Q = RW * NC / 4 / NT;
+      constexpr int Q = WR * NC / 4 / 64;
       const size_t mbase = ((size_t)f * ns + r0) * NC;
-      const int tid = rr * P + t;
+      const int lane = opaque(lane0);
 #pragma unroll
       for (int i = 0; i < Q; ++i) {
-        const int e = 4 * (tid + NT * i);
+        const int e = 4 * (lane + 64 * i);
         const int rl = e / NC, d = e - rl * NC;
         const float* mr = mags + rl * REGM + pad16(d);  // d % 4 == 0: 4 floats in one 16-block
         const float4 v = make_float4(mr[0], mr[1], mr[2], mr[3]);
@@ -610,11 +630,8 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
         }
       }
     }
-    if (cf.enabled)
-      // the FFT rows are free now: they hold the detection cell list (RW*NC <= 2*RW*REGD)
-      cfar1d_dispatch<NC, NT>(mags, REGM, rr, t, r0, frame0 + f, tile0 + tile, cf, sink, s_scan,
-                              reinterpret_cast<uint32_t*>(lds));
-    __syncthreads();  // mags / lds reused by the next tile
+    if (cf.enabled) cfar1d_dispatch<NC>(mags, list, rr, t, r0, frame0 + f, tile0 + tile, cf, sink);
+    pass_sync<false>();  // the region is reused by the next tile
   }
 }
 

@@ -42,6 +42,7 @@ def main():
         "bare": dict(cfar="none", map=False, chunk=0, mti=False),
         "os2d": dict(cfar="os2d", map=True, chunk=0, mti=False),
         "chunk16": dict(cfar="os1d", map=True, chunk=16, mti=False),
+        "chunk32": dict(cfar="os1d", map=True, chunk=32, mti=False),
         "chunk64": dict(cfar="os1d", map=True, chunk=64, mti=False),
         "chunk128": dict(cfar="os1d", map=True, chunk=128, mti=False),
         "chunk256": dict(cfar="os1d", map=True, chunk=256, mti=False),

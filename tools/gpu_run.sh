@@ -30,6 +30,7 @@ for s in "$@"; do
     counters) run counters 120 rocprofv3 -L ;;
     pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_LDS_BANK_CONFLICT -d "$OUT/pmc_sq" -o run --output-format csv -- python3 tools/ablate.py --frames 256 --steps 2 --variants base ;;
     pmc_var_*) v=${s#pmc_var_}; run "pmc_$v" 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/pmc_$v" -o run --output-format csv -- python3 tools/ablate.py --frames 256 --steps 2 --variants "$v" ;;
+    pmc2_var_*) v=${s#pmc2_var_}; run "pmc2_$v" 600 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_BUSY_CYCLES SQ_WAVES -d "$OUT/pmc2_$v" -o run --output-format csv -- python3 tools/ablate.py --frames 256 --steps 2 --variants "$v" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
