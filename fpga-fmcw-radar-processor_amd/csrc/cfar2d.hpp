@@ -1,25 +1,29 @@
 // cfar2d.hpp -- K3: 2-D OS-CFAR (rtl/src/os_cfar_2d.vhd:140-217) over the linear magnitude
-// map, for gfx950.  Included by kernels.hpp (needs DetSink, det_reserve, block_excl_scan1).
+// map, for gfx950.  Included from inside namespace fmcw by kernels.hpp (uses DetSink,
+// det_reserve_wave, wave_excl_scan, lt_bit, opaque, the magnitude-row format midx / moff /
+// mrow_floats / load_cells and DopplerGeom declared there).
 //
-// One workgroup = TR = 4096/NC CUT rows x all NC Doppler cells of one frame; rows
-// r0-hr .. r0+TR-1+hr sit in LDS, each row padded one float per 16 (index pad16(d)), so
-// lanes that start 16 cells apart hit distinct banks.  Doppler is circular; a CUT row is
-// tested only if its whole range extent lies inside the map (build spec).
+// Tiles.  The detection unit is K2's wave tile: WR = 1024/NC range rows x NC Doppler cells
+// (16 cells per lane), so the 1-D and 2-D CFAR share one sink layout and one (frame, range,
+// doppler) order.  A workgroup (4 waves) takes 4 consecutive wave tiles of one frame and
+// stages their rows plus +-hr halo rows in LDS once, in the magnitude-row format (16-cell
+// circular Doppler halos, 4 pad floats per 16 cells).  After that the waves run on their own.
+// Doppler is circular; a CUT row is tested only if its whole range extent lies inside the map
+// (build spec).
 //
-// Phase A (every cell): thread t owns 16 consecutive cells of one row.  For each of the
-// 2 hr + 1 window rows it loads that row's 16 + 2 hd span once, scales it by s_min, and
-// counts for each of its 16 CUTs the refs with fl(s_min * ref) >= cut (guard rows skip
-// |dd| <= gd).  #{..} >= n_ref - k proves cut <= fl(s * ranked) for every admissible scale
-// s >= s_min, so the cell cannot detect; the rest (survivors) go to a bitmap.
-// Phase B (survivors, in (row, doppler) order): one whole wave per cell.  Lanes hold refs
-// l and l + 64 (fixed order: dr outer, dd inner); the mean is the fixed fp32 halving tree
-// (one add + xor-shuffles 32..1 == oracle tree_sum_f32); the scale bracket from ballot counts
-// (ranked > M <=> #{ref > M} >= n_ref - k; ranked < M' <=> #{ref < M'} >= k + 1); detect
-// <=> #{fl(s * ref) >= cut} < n_ref - k; for detections the exact ranked value by a 32-step
-// radix select over order-preserving keys (threshold = fl(s * ranked), dbg_threshold).
-//
-// Included from inside namespace fmcw by kernels.hpp (uses DetSink, det_reserve,
-// block_excl_scan1, opaque, pad16 declared there).
+// Phase A (every cell, one lane per 16 consecutive cells): for each of the 2 hr + 1 window
+// rows the lane reads that row's 16 + 2 hd span once (16-B LDS reads), scales it by s_min,
+// and counts for each of its 16 CUTs the refs with fl(s_min * ref) < cut (guard rows skip
+// |dd| <= gd).  #{fl(s_min * ref) >= cut} >= n_ref - k proves cut <= fl(s * ranked) for
+// every admissible scale s >= s_min, so such a cell cannot detect; the others are candidates.
+// Phase B (candidates, one whole wave per cell, in cell order): lanes hold refs l and l + 64
+// (fixed order: dr outer, dd inner); the mean is the fixed fp32 halving tree (one add, then
+// xor-shuffles 32..1 == oracle tree_sum_f32); the scale bracket comes from ballot counts
+// (ranked > M <=> #{ref > M} >= n_ref - k; ranked < M' <=> #{ref < M'} >= k + 1); detect <=>
+// #{fl(s * ref) >= cut} < n_ref - k.  Pass 1 decides and counts, the wave reserves its sink
+// range, pass 2 walks its detections again and finds the exact ranked value by a 32-step radix
+// select over order-preserving keys (threshold = fl(s * ranked), dbg_threshold).  No per-cell
+// list is kept, so LDS holds only the rows.
 #pragma once
 
 struct Cfar2DArgs {
@@ -31,10 +35,11 @@ struct Cfar2DArgs {
 
 template <int NC> struct Cfar2DGeom {
   static constexpr int NT = 256;
-  static constexpr int TR = 4096 / NC;   // CUT rows per workgroup (4096 cells, 16 per thread)
-  static constexpr int CW = 4096 / 4;    // cells per wave
-  static constexpr int RS = padded(NC);  // LDS row stride (floats)
-  static constexpr int TPR = NC / 16;    // threads per row
+  static constexpr int WPB = 4;                   // wave tiles per workgroup tile
+  static constexpr int WR = DopplerGeom<NC>::WR;  // CUT rows per wave tile
+  static constexpr int TR = WPB * WR;             // CUT rows per workgroup tile
+  static constexpr int RS = mrow_floats<NC>();    // LDS row stride (floats)
+  static constexpr int TPR = NC / 16;             // lanes per row
 };
 
 __device__ __forceinline__ uint32_t f2key(float f) {
@@ -48,30 +53,36 @@ __device__ __forceinline__ float key2f(uint32_t k) {
 template <int NC>
 constexpr size_t cfar2d_smem_bytes(int hr) {
   using G = Cfar2DGeom<NC>;
-  return (size_t)(G::TR + 2 * hr) * G::RS * 4      // tile
-         + (size_t)G::TR * NC / 16 * 2               // survivor bitmap (u16 per 16 cells)
-         + 4 * (size_t)G::CW * 8                     // per-wave detection lists
-         + 128 * 4 + 16 * 4;                         // offsets, scan scratch
+  return (size_t)(G::TR + 2 * hr) * G::RS * 4;
 }
 
-// Phase A for a compile-time Doppler extent HD / guard GD; returns this thread's survivor bits.
+// Phase A for a compile-time Doppler extent HD / guard GD; returns this lane's candidate bits.
+// `rl` is the CUT row within the workgroup tile (tile row rl + hr).
 template <int NC, int HD, int GD>
 __device__ __forceinline__ uint32_t cfar2d_phase_a(const float* tile, int rl, int d0, const Cfar2DArgs& a,
                                                    int need) {
   constexpr int RS = Cfar2DGeom<NC>::RS;
+  static_assert(HD <= MH, "the window stays inside the row halos");
   constexpr int W = 16 + 2 * HD;
-  const float* crow = tile + (rl + a.hr) * RS;
+  constexpr int O0 = floor4(-HD);
+  constexpr int NV = (W + (-HD - O0) + 3) / 4;
+  const float* lb = tile + (rl + a.hr) * RS + midx(d0);
   uint32_t cb[16], lt[16];   // cut bits; #{fl(s_min * ref) < cut} (lt_bit: no SGPR masks)
+  {
+    float c[16];
+    load_cells<4>(lb, 0, c);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    cb[i] = __float_as_uint(crow[pad16(d0 + i)]);
-    lt[i] = 0;
+    for (int i = 0; i < 16; ++i) {
+      cb[i] = __float_as_uint(c[i]);
+      lt[i] = 0;
+    }
   }
   for (int dr = -a.hr; dr <= a.hr; ++dr) {
-    const float* row = crow + dr * RS;
+    float v[4 * NV];
+    load_cells<NV>(lb + dr * RS, O0, v);
     uint32_t sb[W];
 #pragma unroll
-    for (int k = 0; k < W; ++k) sb[k] = __float_as_uint(a.s_min * row[pad16((d0 - HD + k) & (NC - 1))]);
+    for (int k = 0; k < W; ++k) sb[k] = __float_as_uint(a.s_min * v[-HD - O0 + k]);
     if (dr >= -a.gr && dr <= a.gr) {  // guard row: skip |dd| <= GD (uniform branch)
 #pragma unroll
       for (int i = 0; i < 16; ++i)
@@ -85,14 +96,14 @@ __device__ __forceinline__ uint32_t cfar2d_phase_a(const float* tile, int rl, in
         for (int dd = -HD; dd <= HD; ++dd) lt[i] += lt_bit(sb[i + HD + dd], cb[i]);
     }
   }
-  // survivor <=> #{fl(s_min * ref) >= cut} < need  <=>  lt > n_ref - need
+  // candidate <=> #{fl(s_min * ref) >= cut} < need  <=>  lt > n_ref - need
   uint32_t bits = 0;
 #pragma unroll
   for (int i = 0; i < 16; ++i) bits |= ((int)lt[i] > a.n_ref - need ? 1u : 0u) << i;
   return bits;
 }
 
-// Phase A, runtime geometry (any window the LDS budget allows).
+// Phase A, runtime geometry (any window the LDS budget allows; Doppler wraps explicitly).
 template <int NC>
 __device__ __forceinline__ uint32_t cfar2d_phase_a_generic(const float* tile, int rl, int d0,
                                                            const Cfar2DArgs& a, int need) {
@@ -101,14 +112,14 @@ __device__ __forceinline__ uint32_t cfar2d_phase_a_generic(const float* tile, in
   uint32_t bits = 0;
   for (int i = 0; i < 16; ++i) {
     const int d = d0 + i;
-    const uint32_t c = __float_as_uint(crow[pad16(d)]);
+    const uint32_t c = __float_as_uint(crow[midx(d)]);
     uint32_t lt = 0;
     for (int dr = -a.hr; dr <= a.hr; ++dr) {
       const float* row = crow + dr * RS;
       const bool grow = dr >= -a.gr && dr <= a.gr;
       for (int dd = -a.hd; dd <= a.hd; ++dd) {
         if (grow && dd >= -a.gd && dd <= a.gd) continue;
-        lt += lt_bit(__float_as_uint(a.s_min * row[pad16((d + dd) & (NC - 1))]), c);
+        lt += lt_bit(__float_as_uint(a.s_min * row[midx((d + dd) & (NC - 1))]), c);
       }
     }
     bits |= ((int)lt > a.n_ref - need ? 1u : 0u) << i;
@@ -116,141 +127,185 @@ __device__ __forceinline__ uint32_t cfar2d_phase_a_generic(const float* tile, in
   return bits;
 }
 
+// Reference j of the fixed order (dr ascending outer, dd ascending inner, guard block
+// skipped; oracle cfar2d_offsets) -> (dr, dd).  Run once per lane per kernel.
+__device__ __forceinline__ void cfar2d_ref_offset(const Cfar2DArgs& a, int j, int& dr, int& dd) {
+  dr = 0;
+  dd = 0;
+  int n = 0;
+  for (int r = -a.hr; r <= a.hr; ++r) {
+    const bool grow = r >= -a.gr && r <= a.gr;
+    const int side = a.hd - a.gd;
+    const int cnt = grow ? 2 * side : 2 * a.hd + 1;
+    if (j < n + cnt) {
+      const int k = j - n;
+      dr = r;
+      dd = grow ? (k < side ? -a.hd + k : a.gd + 1 + (k - side)) : -a.hd + k;
+      return;
+    }
+    n += cnt;
+  }
+}
+
 template <int NC, int HD, int GD>
 __global__ void __launch_bounds__(256)
-k_cfar2d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int tile0, Cfar2DArgs a,
+k_cfar2d(const float* __restrict__ map, int ns, int n_wg_tiles, int frame0, int tile0, Cfar2DArgs a,
          DetSink sink) {
   using Gm = Cfar2DGeom<NC>;
-  constexpr int TR = Gm::TR, CW = Gm::CW, NT = Gm::NT, RS = Gm::RS, TPR = Gm::TPR;
+  constexpr int WR = Gm::WR, NT = Gm::NT, RS = Gm::RS, TPR = Gm::TPR, WPB = Gm::WPB;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int rows_in = TR + 2 * a.hr;
-  float* tile = smem;
-  uint16_t* surv = reinterpret_cast<uint16_t*>(tile + rows_in * RS);
-  uint2* lists = reinterpret_cast<uint2*>(surv + TR * NC / 16);     // 8-B aligned: TR*NC/16*2 % 8 == 0
-  short2* offs = reinterpret_cast<short2*>(lists + 4 * CW);
-  int* s_scan = reinterpret_cast<int*>(offs + 128);
+  float* const tile = smem;
 
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  // reference-cell offsets in the fixed order (dr outer, dd inner, guard skipped)
-  if (threadIdx.x == 0) {
-    int n = 0;
-    for (int dr = -a.hr; dr <= a.hr; ++dr)
-      for (int dd = -a.hd; dd <= a.hd; ++dd) {
-        if (dr >= -a.gr && dr <= a.gr && dd >= -a.gd && dd <= a.gd) continue;
-        offs[n++] = make_short2((short)dr, (short)dd);
-      }
-  }
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // this lane's two reference cells (index lane and lane + 64 of the fixed order)
+  int dra, dda, drb, ddb;
+  cfar2d_ref_offset(a, lane, dra, dda);
+  cfar2d_ref_offset(a, lane + 64, drb, ddb);
+  const bool oka = lane < a.n_ref, okb = lane + 64 < a.n_ref;
+  const int offa = dra * RS, offb = drb * RS;
   const int need = a.n_ref - a.rank;
-  const int tiles_per_frame = (ns + TR - 1) / TR;
+  const int wt_per_frame = ns / WR;                      // wave tiles per frame
+  const int wg_per_frame = (wt_per_frame + WPB - 1) / WPB;
 
-  for (int tl = blockIdx.x; tl < n_tiles; tl += gridDim.x) {
+  for (int g = blockIdx.x; g < n_wg_tiles; g += gridDim.x) {
+    const int f = g / wg_per_frame;
+    const int wt0 = (g - f * wg_per_frame) * WPB;        // first wave tile of this group
+    const int n_wt = min(WPB, wt_per_frame - wt0);
+    const int r0 = wt0 * WR;                             // first CUT row of this group
+    const int rows_in = n_wt * WR + 2 * a.hr;
     const int tid = opaque(threadIdx.x);
-    const int f = tl / tiles_per_frame;
-    const int r0 = (tl - f * tiles_per_frame) * TR;
-    __syncthreads();
-    // load rows r0-hr .. r0+TR+hr-1 (zero outside the map), padded
-    const float* fm = map + (size_t)f * ns * NC;
-    for (int e = 4 * tid; e < rows_in * NC; e += 4 * NT) {
-      const int rl = e / NC, d = e - rl * NC;
-      const int r = r0 - a.hr + rl;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (r >= 0 && r < ns) v = *reinterpret_cast<const float4*>(fm + (size_t)r * NC + d);
-      float* dst = tile + rl * RS + pad16(d);  // d % 4 == 0: the 4 floats share a 16-block
-      dst[0] = v.x;
-      dst[1] = v.y;
-      dst[2] = v.z;
-      dst[3] = v.w;
-    }
-    __syncthreads();
-
-    // Phase A
+    __syncthreads();  // the previous group's waves are done with the rows
     {
-      const int rl = tid / TPR, d0 = (tid % TPR) * 16;
-      const int r = r0 + rl;
-      uint32_t bits = 0;
-      if (r >= a.hr && r < ns - a.hr) {
-        if constexpr (HD > 0)
-          bits = cfar2d_phase_a<NC, HD, GD>(tile, rl, d0, a, need);
-        else
-          bits = cfar2d_phase_a_generic<NC>(tile, rl, d0, a, need);
+      // rows r0-hr .. r0+n_wt*WR+hr-1 (zero outside the map), 4 float4 loads in flight per lane
+      const float* fm = map + (size_t)f * ns * NC;
+      const int n4 = rows_in * (NC / 4);
+      for (int b = tid; b < n4; b += 4 * NT) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e4 = b + u * NT;
+          const int rl = e4 / (NC / 4), d = (e4 - rl * (NC / 4)) * 4;
+          const int r = r0 - a.hr + rl;
+          v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (e4 < n4 && r >= 0 && r < ns) v[u] = *reinterpret_cast<const float4*>(fm + (size_t)r * NC + d);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e4 = b + u * NT;
+          if (e4 < n4) {
+            const int rl = e4 / (NC / 4), d = (e4 - rl * (NC / 4)) * 4;
+            *reinterpret_cast<float4*>(tile + rl * RS + midx(d)) = v[u];
+          }
+        }
       }
-      surv[tid] = (uint16_t)bits;  // word tid covers cells tid*16 .. tid*16+15
     }
     __syncthreads();
+    for (int e = tid; e < rows_in * 2 * MH; e += NT) {   // circular Doppler halos
+      const int rl = e / (2 * MH), j = e - rl * (2 * MH);
+      const int dst = j < MH ? NC + j : j - 2 * MH;
+      const int src = j < MH ? j : NC + j - 2 * MH;
+      tile[rl * RS + midx(dst)] = tile[rl * RS + midx(src)];
+    }
+    __syncthreads();
+    if (wv >= n_wt) continue;  // uniform per wave: no wave tile left in this frame
 
-    // Phase B: wave wv walks its 64 words (= its 1024 cells) in cell order
-    int ndet = 0;
-    uint2* mylist = lists + wv * CW;
-    const uint32_t word = surv[wv * 64 + lane];
-    uint64_t nz = __ballot(word != 0);
+    // ---- Phase A: candidates among this lane's 16 cells
+    const int rlw = wv * WR + lane / TPR;    // CUT row within the group tile
+    const int d0 = (lane % TPR) * 16;
+    const int r = r0 + rlw;
+    uint32_t cand = 0;
+    if (r >= a.hr && r < ns - a.hr) {
+      if constexpr (HD > 0)
+        cand = cfar2d_phase_a<NC, HD, GD>(tile, rlw, d0, a, need);
+      else
+        cand = cfar2d_phase_a_generic<NC>(tile, rlw, d0, a, need);
+    }
+
+    // ---- Phase B helpers: the wave's view of candidate cell (row l0 / TPR of the wave, d)
+    auto refs_of = [&](int l0, int d, float& va, float& vb) {
+      const float* crow = tile + (wv * WR + l0 / TPR + a.hr) * RS;
+      va = oka ? crow[offa + midx((d + dda) & (NC - 1))] : 0.f;
+      vb = okb ? crow[offb + midx((d + ddb) & (NC - 1))] : 0.f;
+    };
+    auto scale_of = [&](float va, float vb) -> float {
+      float sum = va + vb;
+#pragma unroll
+      for (int x = 32; x >= 1; x >>= 1) sum += __shfl_xor(sum, x, 64);
+      const float mean = sum / (float)a.n_ref;
+      if (a.override_) return (float)a.override_;
+      const float half = mean * 0.5f;
+      const float hi = mean + half;
+      const int n_hi = __popcll(__ballot(oka && va > hi)) + __popcll(__ballot(okb && vb > hi));
+      const int n_lo = __popcll(__ballot(oka && va < half)) + __popcll(__ballot(okb && vb < half));
+      return (n_hi >= need) ? a.sc_max : (n_lo >= a.rank + 1) ? a.sc_min : a.sc_nom;
+    };
+
+    // ---- Phase B pass 1: decide every candidate (cell order); detections -> owner's bits
+    uint32_t detw = 0;
+    {
+      uint64_t nz = __ballot(cand != 0);
+      while (nz) {
+        const int l0 = __builtin_ctzll(nz);
+        nz &= nz - 1;
+        uint32_t bits = (uint32_t)__shfl((int)cand, l0, 64);
+        while (bits) {
+          const int i = __builtin_ctz(bits);
+          bits &= bits - 1;
+          const int d = (l0 % TPR) * 16 + i;
+          const float cut = tile[(wv * WR + l0 / TPR + a.hr) * RS + midx(d)];
+          float va, vb;
+          refs_of(l0, d, va, vb);
+          const float sc = scale_of(va, vb);
+          const int n_ge = __popcll(__ballot(oka && sc * va >= cut)) + __popcll(__ballot(okb && sc * vb >= cut));
+          if (n_ge < need && lane == l0) detw |= 1u << i;
+        }
+      }
+    }
+    int total;
+    (void)wave_excl_scan(__popc(detw), total);
+    const int wtile = tile0 + f * wt_per_frame + wt0 + wv;
+    const uint32_t base = det_reserve_wave(sink, wtile, total);
+
+    // ---- Phase B pass 2: exact ranked value (k-th smallest) of each detection, in order
+    uint32_t o = 0;
+    uint64_t nz = __ballot(detw != 0);
     while (nz) {
       const int l0 = __builtin_ctzll(nz);
       nz &= nz - 1;
-      uint32_t bits = (uint32_t)__shfl((int)word, l0, 64);
+      uint32_t bits = (uint32_t)__shfl((int)detw, l0, 64);
       while (bits) {
         const int i = __builtin_ctz(bits);
         bits &= bits - 1;
-        const int cell = (wv * 64 + l0) * 16 + i;
-        const int rl = cell / NC, d = cell - rl * NC;
-        const float* crow = tile + (rl + a.hr) * RS;
-        const float cut = crow[pad16(d)];
-        float va = 0.f, vb = 0.f;
-        const bool oka = lane < a.n_ref, okb = lane + 64 < a.n_ref;
-        if (oka) { const short2 o = offs[lane]; va = crow[o.x * RS + pad16((d + o.y) & (NC - 1))]; }
-        if (okb) { const short2 o = offs[lane + 64]; vb = crow[o.x * RS + pad16((d + o.y) & (NC - 1))]; }
-        float sum = va + vb;
-#pragma unroll
-        for (int x = 32; x >= 1; x >>= 1) sum += __shfl_xor(sum, x, 64);
-        const float mean = sum / (float)a.n_ref;
-        float sc;
-        if (a.override_) {
-          sc = (float)a.override_;
-        } else {
-          const float half = mean * 0.5f;
-          const float hi = mean + half;
-          const int n_hi = __popcll(__ballot(oka && va > hi)) + __popcll(__ballot(okb && vb > hi));
-          const int n_lo = __popcll(__ballot(oka && va < half)) + __popcll(__ballot(okb && vb < half));
-          sc = (n_hi >= need) ? a.sc_max : (n_lo >= a.rank + 1) ? a.sc_min : a.sc_nom;
-        }
-        const int n_ge = __popcll(__ballot(oka && sc * va >= cut)) + __popcll(__ballot(okb && sc * vb >= cut));
-        if (n_ge < need) {
-          // exact k-th smallest (k = rank) by radix select on order keys
-          const uint32_t ka = f2key(va), kb = f2key(vb);
-          uint32_t prefix = 0;
-          int k = a.rank;
-          for (int bit = 31; bit >= 0; --bit) {
-            const uint32_t hmask = bit == 31 ? 0u : ~((2u << bit) - 1u);
-            const bool za = oka && ((ka & hmask) == prefix) && !((ka >> bit) & 1u);
-            const bool zb = okb && ((kb & hmask) == prefix) && !((kb >> bit) & 1u);
-            const int c0 = __popcll(__ballot(za)) + __popcll(__ballot(zb));
-            if (k >= c0) {
-              k -= c0;
-              prefix |= 1u << bit;
-            }
+        const int d = (l0 % TPR) * 16 + i;
+        const int rl = wv * WR + l0 / TPR;
+        float va, vb;
+        refs_of(l0, d, va, vb);
+        const float sc = scale_of(va, vb);
+        const uint32_t ka = f2key(va), kb = f2key(vb);
+        uint32_t prefix = 0;
+        int k = a.rank;
+        for (int bit = 31; bit >= 0; --bit) {
+          const uint32_t hmask = bit == 31 ? 0u : ~((2u << bit) - 1u);
+          const bool za = oka && ((ka & hmask) == prefix) && !((ka >> bit) & 1u);
+          const bool zb = okb && ((kb & hmask) == prefix) && !((kb >> bit) & 1u);
+          const int c0 = __popcll(__ballot(za)) + __popcll(__ballot(zb));
+          if (k >= c0) {
+            k -= c0;
+            prefix |= 1u << bit;
           }
-          if (lane == 0) mylist[ndet] = make_uint2((uint32_t)cell, __float_as_uint(sc * key2f(prefix)));
-          ++ndet;
         }
-      }
-    }
-    // ordered emission: waves in row order, each list in cell order
-    int total;
-    const int excl = block_excl_scan1<NT>(lane == 0 ? ndet : 0, s_scan, total);
-    const int wexcl = __shfl(excl, 0, 64);
-    const uint32_t base = det_reserve(sink, tile0 + tl, total, s_scan + NT / 64 + 1);
-    for (int i = lane; i < ndet; i += 64) {
-      const uint2 rec = mylist[i];
-      const uint32_t slot = base + (uint32_t)(wexcl + i);
-      if (slot < sink.cap) {
-        const int cell = (int)rec.x;
-        const int rl = cell / NC, d = cell - rl * NC;
-        fmcw_det dd;
-        dd.frame = (uint32_t)(frame0 + f);
-        dd.range = (uint16_t)(r0 + rl);
-        dd.doppler = (uint16_t)d;
-        dd.mag = tile[(rl + a.hr) * RS + pad16(d)];
-        dd.threshold = __uint_as_float(rec.y);
-        sink.scratch[slot] = dd;
+        const uint32_t slot = base + o;
+        if (lane == 0 && slot < sink.cap) {
+          fmcw_det dd;
+          dd.frame = (uint32_t)(frame0 + f);
+          dd.range = (uint16_t)(r0 + rl);
+          dd.doppler = (uint16_t)d;
+          dd.mag = tile[(rl + a.hr) * RS + midx(d)];
+          dd.threshold = sc * key2f(prefix);
+          sink.scratch[slot] = dd;
+        }
+        ++o;
       }
     }
   }

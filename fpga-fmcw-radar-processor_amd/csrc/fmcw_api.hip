@@ -321,12 +321,9 @@ DetSink make_sink(fmcw_handle* h) {
   return s;
 }
 
+// Detection tiles per frame: K2's wave tiles (WR range rows), shared by the 1-D and 2-D CFAR.
 size_t tiles_per_frame(const fmcw_handle* h) {
   const fmcw_config& c = h->cfg;
-  if (c.cfar_kind == FMCW_CFAR_OS2D) {
-    const int tr = cfar2_info(c.n_doppler).TR;
-    return (c.n_range + tr - 1) / tr;
-  }
   return c.n_range / doppler_info(c.n_doppler).WR;
 }
 
@@ -338,11 +335,12 @@ int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipS
   if (c.cfar_kind == FMCW_CFAR_OS2D) {
     const Cfar2DArgs a = cfar2_args(c);
     const Cfar2Info ci = cfar2_info(c.n_doppler, a.hd, a.gd);
-    const int n_tiles = nf * (int)tiles_per_frame(h);
-    const int grid = std::min(n_tiles, h->grid_cfar);
+    // workgroup tiles: 4 consecutive wave tiles of one frame
+    const int n_wg_tiles = nf * (int)((tiles_per_frame(h) + 3) / 4);
+    const int grid = std::min(n_wg_tiles, h->grid_cfar);
     ProfScope ps(h, FMCW_K_CFAR2D, s);
     hipLaunchKernelGGL(ci.fn, dim3(grid), dim3(256), h->cfar2d_smem, s, map_chunk, (int)c.n_range,
-                       n_tiles, frame0, tile0, a, sink);
+                       n_wg_tiles, frame0, tile0, a, sink);
     return check_launch("k_cfar2d");
   }
   // 1-D on a caller map (fmcw_cfar); inside fmcw_enqueue the 1-D CFAR is fused into K2
@@ -516,7 +514,7 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   if (c.cfar_kind == FMCW_CFAR_OS2D) {
     const Cfar2DArgs a = cfar2_args(c);
     h->cfar2d_smem = cfar2_smem(c.n_doppler, a.hr);
-    const Cfar2Info ci = cfar2_info(c.n_doppler);
+    const Cfar2Info ci = cfar2_info(c.n_doppler, a.hd, a.gd);  // the kernel launch_cfar runs
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(ci.fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)h->cfar2d_smem) != hipSuccess)
       (void)hipGetLastError();

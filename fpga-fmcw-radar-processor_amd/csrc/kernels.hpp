@@ -260,6 +260,48 @@ struct Cfar1DArgs {
 };
 
 // --------------------------------------------------------------------------------------
+// Magnitude rows in LDS (K2, the 1-D CFAR and K3).  A row holds the NC cells plus a 16-cell
+// circular halo on each side (cells -16..-1 = NC-16..NC-1, cells NC..NC+15 = 0..15), so a
+// CFAR window of reach <= 16 never wraps and its addresses are a per-lane base plus
+// immediates.  Every 16 cells are followed by 4 pad floats: each 16-cell block starts 16-B
+// aligned (one ds_read_b128 per 4 cells) and 16 lanes reading blocks 16 cells apart touch 16
+// disjoint bank quads (20 t mod 64 are distinct).
+// --------------------------------------------------------------------------------------
+constexpr int MH = 16;  // halo cells per side
+__host__ __device__ constexpr int midx(int d) { return (d + MH) + (((d + MH) >> 4) << 2); }
+// midx(x + o) - midx(x) for x % 16 == 0 and a compile-time o >= -MH
+__host__ __device__ constexpr int moff(int o) { return o + 4 * (o >= 0 ? o / 16 : -((15 - o) / 16)); }
+// midx(x + o) - midx(x) for o >= 0 when x % 16 + o % 16 < 16 (cf. padoff)
+__host__ __device__ constexpr int mpadoff(int o) { return o + 4 * (o / 16); }
+template <int NC> constexpr int mrow_floats() { return (((NC + 2 * MH) * 5 / 4) + 3) & ~3; }
+__host__ __device__ constexpr int floor4(int x) { return x >= 0 ? x & ~3 : -((-x + 3) & ~3); }
+
+// Fill the circular halos of one magnitude row once its NC cells are written; the P lanes
+// that share the row copy cells j = t, t + P, ... of the 32 halo cells.
+template <int NC, int P>
+__device__ __forceinline__ void fill_halo(float* row, int t) {
+  for (int j = t; j < 2 * MH; j += P) {
+    const int dst = j < MH ? NC + j : j - 2 * MH;
+    const int src = j < MH ? j : NC + j - 2 * MH;
+    row[midx(dst)] = row[midx(src)];
+  }
+}
+
+// Cells [o0, o0 + 4 NV) of a row relative to a 16-cell-aligned lane base (o0 % 4 == 0), as NV
+// 16-byte LDS reads.
+template <int NV>
+__device__ __forceinline__ void load_cells(const float* base, int o0, float (&v)[4 * NV]) {
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const float4 q = *reinterpret_cast<const float4*>(base + moff(o0 + 4 * c));
+    v[4 * c] = q.x;
+    v[4 * c + 1] = q.y;
+    v[4 * c + 2] = q.z;
+    v[4 * c + 3] = q.w;
+  }
+}
+
+// --------------------------------------------------------------------------------------
 // Wave tiles.  K2 and the stand-alone 1-D CFAR work on tiles of WR = 64 / P range rows x all
 // NC Doppler cells of one frame (P = NC/16 lanes per row, 16 cells per lane), ONE WAVEFRONT
 // per tile: a row's Doppler FFT, its magnitudes, its CFAR window and its detection list all
@@ -268,18 +310,21 @@ struct Cfar1DArgs {
 // arithmetic (a workgroup is only the unit of LDS allocation).  A tile is also the unit of
 // detection ordering (DetSink tile = (frame, range rows)).
 // --------------------------------------------------------------------------------------
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
 template <int NC> struct DopplerGeom {
   static constexpr int P = NC / 16;                     // lanes per range row (16 cells each)
   static constexpr int WR = 64 / P;                     // range rows per wave tile
   static constexpr int WPB = 4;                         // waves per workgroup (independent)
   static constexpr int NT = 64 * WPB;
   static constexpr int REGD = padded(NC) + 4;           // complex per range row (FFT)
-  static constexpr int REGM = padded(NC);               // floats per range row (magnitudes)
-  static constexpr int WREG = WR * REGD;                // complex per wave region
+  static constexpr int REGM = mrow_floats<NC>();        // floats per magnitude row
+  static constexpr int LIST = WR * REGM;                // detection cell list (u32) offset
+  // floats per wave region: the FFT rows, later the magnitude rows + the cell list
+  static constexpr int WFL = cmax(2 * WR * REGD, LIST + WR * NC);
   static constexpr int LR = FinalRadix<NC, 16>::R;      // last pass radix (after pass 1)
   static constexpr int LG = 16 / LR;
-  // the magnitudes and then the detection cell list reuse the wave's FFT rows
-  static_assert(WR * REGM + WR * NC <= 2 * WREG, "magnitudes + cell list fit the wave region");
+  static_assert(WFL % 4 == 0 && REGM % 4 == 0, "16-B aligned rows and regions");
 };
 
 // Wave-level exclusive scan (shuffles only); `total` = the wave's sum, uniform.
@@ -315,20 +360,11 @@ __device__ __forceinline__ uint32_t det_reserve_wave(const DetSink& sink, int ti
   return base;
 }
 
-// 1-D OS-CFAR along Doppler (circular) over a wave tile's magnitude rows (row stride
-// padded(NC) floats, index pad16(d)), plus ordered emission.  Lane (rr, t) tests the 16
-// consecutive cells d0 = 16 t .. d0 + 15 of row rr, so emission in lane order is (range,
-// doppler) order.  detect <=> #{refs : fl(alpha*ref) >= cut} < n_ref - rank  <=>
-// #{fl(alpha*ref) < cut} > rank, which is cut > fl(alpha * sorted(refs)[rank])
-// (rtl/old/os_cfar.vhd:330-369) without a sort.  The count is mask-free integer arithmetic
-// (lt_bit) so that hundreds of compares do not become SGPR masks that spill.
-// REF > 0: compile-time geometry (REF refs + GUARD guards per side) with the whole window in
-// registers; REF == 0: runtime geometry read from LDS.
+// exact k-th smallest of 2*REF registers: bitonic sort (compile-time indices), then the max of
+// the ascending prefix r[0..rank] (a select chain `i == rank ? r[i] : out` is turned by LLVM
+// into a private-array lookup, i.e. a scratch store + indexed load per detection)
 template <int REF, int GUARD>
 __device__ __forceinline__ float ranked_of(float (&r)[2 * REF], int rank) {
-  // exact k-th smallest of 2*REF registers: bitonic sort (compile-time indices), then the
-  // max of the ascending prefix r[0..rank] (a select chain `i == rank ? r[i] : out` is turned
-  // by LLVM into a private-array lookup, i.e. a scratch store + indexed load per detection)
   constexpr int N = 2 * REF;
   static_assert((N & (N - 1)) == 0, "power-of-two reference count");
 #pragma unroll
@@ -351,47 +387,97 @@ __device__ __forceinline__ float ranked_of(float (&r)[2 * REF], int rank) {
   return out;
 }
 
+// 1-D OS-CFAR along Doppler (circular) over a wave tile's magnitude rows, plus ordered
+// emission.  Lane (rr, t) tests the 16 consecutive cells d0 = 16 t .. d0 + 15 of row rr, so
+// emission in lane order is (range, doppler) order.  detect <=> #{refs : fl(alpha*ref) >= cut}
+// < n_ref - rank  <=>  #{fl(alpha*ref) < cut} > rank, which is cut > fl(alpha *
+// sorted(refs)[rank]) (rtl/old/os_cfar.vhd:117-137) without a sort.  The count is mask-free
+// integer arithmetic (lt_bit) so that hundreds of compares do not become SGPR masks.
+// REF > 0: compile-time geometry (REF refs + GUARD guards per side) with the window in
+// registers, screened (below); REF == 0: runtime geometry read from LDS.
 template <int NC, int REF, int GUARD>
 __device__ __forceinline__ void cfar1d_wave(const float* mags, uint32_t* list, int rr, int t, int r0,
                                             int frame, int tile, const Cfar1DArgs& cf,
                                             const DetSink& sink) {
   constexpr int CELLS = 16;
-  constexpr int RS = padded(NC);
+  constexpr int RS = DopplerGeom<NC>::REGM;
   const float* mrow = mags + rr * RS;
   const int d0 = t * CELLS;
   const int nref = 2 * cf.ref;
   uint32_t bits = 0;
   if constexpr (REF > 0) {
+    // Screen, then count exactly where needed.  A group of 4 consecutive reference cells
+    // whose minimum satisfies fl(alpha*min) >= cut has all 4 refs at or above cut/alpha
+    // (fl(alpha*x) is monotone in x), so 4 * #{such groups} is a lower bound on
+    // #{refs : fl(alpha*ref) >= cut}; once it reaches need = n_ref - rank the cell cannot
+    // detect.  The exact count (16 compares) runs only for the cell indices where some lane
+    // of the wave survived (a uniform branch) and decides exactly as the unscreened count.
+    static_assert(REF % 4 == 0, "reference runs split into groups of 4");
     constexpr int H = REF + GUARD;
+    static_assert(H <= MH, "the window stays inside the row halos");
+    constexpr int NGS = REF / 4;               // groups of 4 per side
+    constexpr int RO = REF + 2 * GUARD + 1;    // first right ref, relative to the first left ref
     // two halves of 8 cells (a 28-value window each) to keep the register peak low
     constexpr int HC = CELLS / 2, WH = HC + 2 * H;
+    constexpr int NV = (WH + 3 + 3) / 4;       // 16-B reads covering the window from floor4
+    const float* lb = mrow + midx(d0);
+    const int need = nref - cf.rank;
+    const bool one_group = need <= 4;          // the reference (rank 12 of 16): any group rejects
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
-      uint32_t cb[HC], sb[WH];   // cut bits, scaled-window bits
+      const int ws = hh * HC - H;              // first window cell relative to d0
+      const int o0 = floor4(ws);
+      float v[4 * NV];
+      load_cells<NV>(lb, o0, v);
+      float w[WH];
 #pragma unroll
-      for (int k = 0; k < WH; ++k) {
-        const float x = mrow[pad16((d0 + hh * HC - H + k) & (NC - 1))];
-        sb[k] = __float_as_uint(cf.alpha * x);
-        if (k >= H && k < H + HC) cb[k - H] = __float_as_uint(x);
+      for (int k = 0; k < WH; ++k) w[k] = v[ws - o0 + k];
+      float g[WH - 3];                         // g[k] = min(w[k .. k+3])
+      {
+        float m2[WH - 1];
+#pragma unroll
+        for (int k = 0; k < WH - 1; ++k) m2[k] = fminf(w[k], w[k + 1]);
+#pragma unroll
+        for (int k = 0; k < WH - 3; ++k) g[k] = fminf(m2[k], m2[k + 2]);
       }
 #pragma unroll
       for (int i = 0; i < HC; ++i) {
-        uint32_t lt = 0;
+        const float cut = w[H + i];
+        bool surv;
+        if (one_group) {
+          float M = g[i];
 #pragma unroll
-        for (int j = 0; j < REF; ++j)
-          lt += lt_bit(sb[i + j], cb[i]) + lt_bit(sb[i + REF + 2 * GUARD + 1 + j], cb[i]);
-        bits |= ((int)lt > cf.rank ? 1u : 0u) << (hh * HC + i);
+          for (int q = 1; q < NGS; ++q) M = fmaxf(M, g[i + 4 * q]);
+#pragma unroll
+          for (int q = 0; q < NGS; ++q) M = fmaxf(M, g[i + RO + 4 * q]);
+          surv = cf.alpha * M < cut;
+        } else {
+          int ng = 0;
+#pragma unroll
+          for (int q = 0; q < NGS; ++q)
+            ng += (cf.alpha * g[i + 4 * q] >= cut) + (cf.alpha * g[i + RO + 4 * q] >= cut);
+          surv = 4 * ng < need;
+        }
+        if (__any(surv)) {
+          const uint32_t cbits = __float_as_uint(cut);
+          uint32_t lt = 0;
+#pragma unroll
+          for (int j = 0; j < REF; ++j)
+            lt += lt_bit(__float_as_uint(cf.alpha * w[i + j]), cbits) +
+                  lt_bit(__float_as_uint(cf.alpha * w[i + RO + j]), cbits);
+          bits |= ((int)lt > cf.rank ? 1u : 0u) << (hh * HC + i);
+        }
       }
     }
   } else {
 #pragma unroll
     for (int i = 0; i < CELLS; ++i) {
       const int d = d0 + i;
-      const uint32_t c = __float_as_uint(mrow[pad16(d)]);
+      const uint32_t c = __float_as_uint(mrow[midx(d)]);
       uint32_t lt = 0;
       for (int j = 1; j <= cf.ref; ++j) {
-        lt += lt_bit(__float_as_uint(cf.alpha * mrow[pad16((d - cf.guard - j) & (NC - 1))]), c);
-        lt += lt_bit(__float_as_uint(cf.alpha * mrow[pad16((d + cf.guard + j) & (NC - 1))]), c);
+        lt += lt_bit(__float_as_uint(cf.alpha * mrow[midx((d - cf.guard - j) & (NC - 1))]), c);
+        lt += lt_bit(__float_as_uint(cf.alpha * mrow[midx((d + cf.guard + j) & (NC - 1))]), c);
       }
       bits |= ((int)lt > cf.rank ? 1u : 0u) << i;
     }
@@ -417,18 +503,18 @@ __device__ __forceinline__ void cfar1d_wave(const float* mags, uint32_t* list, i
       float r[2 * REF];
 #pragma unroll
       for (int j = 0; j < REF; ++j) {
-        r[j] = row[pad16((d - GUARD - 1 - j) & (NC - 1))];
-        r[REF + j] = row[pad16((d + GUARD + 1 + j) & (NC - 1))];
+        r[j] = row[midx(d - GUARD - 1 - j)];
+        r[REF + j] = row[midx(d + GUARD + 1 + j)];
       }
       ranked = ranked_of<REF, GUARD>(r, cf.rank);
     } else {
       for (int j = 0; j < nref; ++j) {
         const int oj = j < cf.ref ? -(cf.guard + 1 + j) : (cf.guard + 1 + j - cf.ref);
-        const float vj = row[pad16((d + oj) & (NC - 1))];
+        const float vj = row[midx((d + oj) & (NC - 1))];
         int lt = 0, le = 0;
         for (int i2 = 0; i2 < nref; ++i2) {
           const int o2 = i2 < cf.ref ? -(cf.guard + 1 + i2) : (cf.guard + 1 + i2 - cf.ref);
-          const float v2 = row[pad16((d + o2) & (NC - 1))];
+          const float v2 = row[midx((d + o2) & (NC - 1))];
           lt += v2 < vj;
           le += v2 <= vj;
         }
@@ -441,7 +527,7 @@ __device__ __forceinline__ void cfar1d_wave(const float* mags, uint32_t* list, i
       dd.frame = (uint32_t)frame;
       dd.range = (uint16_t)(r0 + rl);
       dd.doppler = (uint16_t)d;
-      dd.mag = row[pad16(d)];
+      dd.mag = row[midx(d)];
       dd.threshold = cf.alpha * ranked;
       sink.scratch[slot] = dd;
     }
@@ -467,10 +553,10 @@ k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int til
          DetSink sink) {
   using Gm = DopplerGeom<NC>;
   constexpr int P = Gm::P, WR = Gm::WR, WPB = Gm::WPB, REGM = Gm::REGM;
-  __shared__ __attribute__((aligned(16))) float2 lds[WPB * Gm::WREG];
+  __shared__ __attribute__((aligned(16))) float lds[WPB * Gm::WFL];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  float* const mags = reinterpret_cast<float*>(lds + wv * Gm::WREG);
-  uint32_t* const list = reinterpret_cast<uint32_t*>(mags + WR * REGM);
+  float* const mags = lds + wv * Gm::WFL;
+  uint32_t* const list = reinterpret_cast<uint32_t*>(mags + Gm::LIST);
   const int tiles_per_frame = ns / WR;
   for (int tile = blockIdx.x * WPB + wv; tile < n_tiles; tile += gridDim.x * WPB) {
     const int lane = opaque(threadIdx.x & 63);
@@ -481,13 +567,10 @@ k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int til
     for (int i = 0; i < WR * NC / 4 / 64; ++i) {
       const int e = 4 * (lane + 64 * i);
       const int rl = e / NC, d = e - rl * NC;
-      const float4 v = *reinterpret_cast<const float4*>(src + e);
-      float* dst = mags + rl * REGM + pad16(d);  // d % 4 == 0: the 4 floats share a 16-block
-      dst[0] = v.x;
-      dst[1] = v.y;
-      dst[2] = v.z;
-      dst[3] = v.w;
+      *reinterpret_cast<float4*>(mags + rl * REGM + midx(d)) = *reinterpret_cast<const float4*>(src + e);
     }
+    pass_sync<false>();
+    fill_halo<NC, P>(mags + (lane / P) * REGM, lane % P);
     pass_sync<false>();
     cfar1d_dispatch<NC>(mags, list, lane / P, lane % P, r0, frame0 + f, tile0 + tile, cf, sink);
     pass_sync<false>();  // the region is reused by the next tile
@@ -512,15 +595,15 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
   constexpr int P = Gm::P, WR = Gm::WR, WPB = Gm::WPB, REGD = Gm::REGD, REGM = Gm::REGM;
   constexpr int LR = Gm::LR, LG = Gm::LG;
   static_assert(P <= 64, "a Doppler transform must fit one wave");
-  __shared__ __attribute__((aligned(16))) float2 lds[WPB * Gm::WREG];
+  __shared__ __attribute__((aligned(16))) float lds[WPB * Gm::WFL];
 
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane0 = threadIdx.x & 63;
   const int rr = lane0 / P;
   const int t0 = lane0 % P;
-  float2* const wreg = lds + wv * Gm::WREG;
-  float* const mags = reinterpret_cast<float*>(wreg);
-  uint32_t* const list = reinterpret_cast<uint32_t*>(mags + WR * REGM);
+  float* const mags = lds + wv * Gm::WFL;
+  float2* const wreg = reinterpret_cast<float2*>(mags);
+  uint32_t* const list = reinterpret_cast<uint32_t*>(mags + Gm::LIST);
   const int tiles_per_frame = ns / WR;
   const int T = 1 << lgT;
   const int lgncb = __builtin_ctz(NC) - lgT;
@@ -603,12 +686,16 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
     float* mrow = mags + rr * REGM;
 #pragma unroll
     for (int g = 0; g < LG; ++g) {
-      float* m0 = mrow + pad16(t + P * g);
+      float* m0 = mrow + midx(t + P * g);
 #pragma unroll
       for (int m = 0; m < LR; ++m)
-        m0[padoff(m * (NC / LR))] = ambm ? acc[g][m] : sqrtf(acc[g][m]);
+        m0[mpadoff(m * (NC / LR))] = ambm ? acc[g][m] : sqrtf(acc[g][m]);
     }
     pass_sync<false>();
+    if (cf.enabled) {
+      fill_halo<NC, P>(mrow, t);
+      pass_sync<false>();
+    }
 
     // map store: WR*NC = 1024 floats contiguous at [f][r0][0], 16 B per lane
     {
@@ -619,8 +706,7 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
       for (int i = 0; i < Q; ++i) {
         const int e = 4 * (lane + 64 * i);
         const int rl = e / NC, d = e - rl * NC;
-        const float* mr = mags + rl * REGM + pad16(d);  // d % 4 == 0: 4 floats in one 16-block
-        const float4 v = make_float4(mr[0], mr[1], mr[2], mr[3]);
+        const float4 v = *reinterpret_cast<const float4*>(mags + rl * REGM + midx(d));
         if (lin_map) *reinterpret_cast<float4*>(lin_map + mbase + e) = v;
         if (db_map) {
           const float k = 6.0205999132796239f;  // 20 / log2(10)

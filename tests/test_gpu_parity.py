@@ -264,12 +264,12 @@ def test_detection_cap_and_errors(gpu):
 
 
 def test_dense_tiles_use_overflow_region(gpu):
-    """Tiles with more detections than their slot (1/16 of the tile's cells) spill into the
+    """Tiles with more detections than their slot (1/32 of the tile's cells) spill into the
     shared overflow region; the list stays complete and in (frame, range, doppler) order."""
     ns, nc, nf = 256, 64, 2
     rng = np.random.default_rng(5)
     m = rng.rayleigh(1.0, (nf, ns, nc)).astype(np.float32)
-    m[0, :64, ::8] = 100.0       # tile 0 of frame 0: 64 rows x 8 spikes = 512 > slot 256
+    m[0, :64, ::8] = 100.0       # each 16-row wave tile: 16 rows x 8 spikes = 128 > slot 32
     m[1, 128:192, 4::8] = 80.0   # a later tile of frame 1
     with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os1d", max_frames=nf) as core:
         got = run_cfar_stage(core, m)

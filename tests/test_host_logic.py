@@ -198,3 +198,35 @@ def test_tiled_corner_turn_layout(ns, nc, T):
         for c in range(nc):
             out[r, c] = inter[((r // rb_ * ncb + c // T) * rb_ + r % rb_) * T + c % T]
     np.testing.assert_array_equal(out, spec.T)
+
+
+def cfar1d_screened(mag, p):
+    """k_doppler's 1-D decision with its screen: a cell whose groups of 4 consecutive refs give
+    4 * #{groups with fl(alpha * min4) >= cut} >= need cannot detect and is never counted; the
+    rest use the exact count.  Returns (detections, screen survivors)."""
+    m = np.asarray(mag, np.float32)
+    a = np.float32(p.alpha)
+    g = np.minimum(np.minimum(m, np.roll(m, -1, -1)), np.minimum(np.roll(m, -2, -1), np.roll(m, -3, -1)))
+    starts = [-(p.guard + p.ref) + 4 * q for q in range(p.ref // 4)] + \
+             [p.guard + 1 + 4 * q for q in range(p.ref // 4)]
+    ng = sum(((a * np.roll(g, -s, -1)) >= m).astype(np.int64) for s in starts)
+    surv = 4 * ng < (2 * p.ref - p.rank)
+    return surv & cfar1d_counting(m, p), surv
+
+
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("rank", [12, 10, 14])
+def test_cfar1d_screen_is_exact(seed, rank):
+    """The groups-of-4 screen never clears a detecting cell (decisions equal the sort)."""
+    rng = np.random.default_rng(50 + seed)
+    mag = rng.rayleigh(1.0, (64, 256)).astype(np.float32)
+    mag[10, 40] = 50.0
+    mag[20, ::7] = 9.0
+    mag[30] = np.float32(2.5)
+    p = O.Cfar1D(rank=rank)
+    det_sort, _ = O.cfar_os1d(mag, p)
+    det, surv = cfar1d_screened(mag, p)
+    np.testing.assert_array_equal(det, det_sort)
+    assert det_sort[10, 40]
+    if rank == 12:
+        assert surv.mean() < 0.05      # the screen clears almost every noise cell
