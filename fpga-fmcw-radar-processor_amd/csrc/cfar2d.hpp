@@ -148,7 +148,7 @@ __device__ __forceinline__ void cfar2d_ref_offset(const Cfar2DArgs& a, int j, in
 }
 
 template <int NC, int HD, int GD>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
 k_cfar2d(const float* __restrict__ map, int ns, int n_wg_tiles, int frame0, int tile0, Cfar2DArgs a,
          DetSink sink) {
   using Gm = Cfar2DGeom<NC>;
@@ -167,10 +167,12 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_wg_tiles, int frame0, int 
   const int need = a.n_ref - a.rank;
   const int wt_per_frame = ns / WR;                      // wave tiles per frame
   const int wg_per_frame = (wt_per_frame + WPB - 1) / WPB;
+  const int nf = n_wg_tiles / wg_per_frame;
 
   for (int g = blockIdx.x; g < n_wg_tiles; g += gridDim.x) {
-    const int f = g / wg_per_frame;
-    const int wt0 = (g - f * wg_per_frame) * WPB;        // first wave tile of this group
+    // frame-minor order (as K2): hot rows (targets) spread over all workgroups
+    const int f = g % nf;
+    const int wt0 = (g / nf) * WPB;                      // first wave tile of this group
     const int n_wt = min(WPB, wt_per_frame - wt0);
     const int r0 = wt0 * WR;                             // first CUT row of this group
     const int rows_in = n_wt * WR + 2 * a.hr;

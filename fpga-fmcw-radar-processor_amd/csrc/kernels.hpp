@@ -558,10 +558,14 @@ k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int til
   float* const mags = lds + wv * Gm::WFL;
   uint32_t* const list = reinterpret_cast<uint32_t*>(mags + Gm::LIST);
   const int tiles_per_frame = ns / WR;
+  const int nf = n_tiles / tiles_per_frame;
   for (int tile = blockIdx.x * WPB + wv; tile < n_tiles; tile += gridDim.x * WPB) {
     const int lane = opaque(threadIdx.x & 63);
-    const int f = tile / tiles_per_frame;
-    const int r0 = (tile - f * tiles_per_frame) * WR;
+    // frame-minor order: consecutive tiles are the same rows of consecutive frames, so the
+    // rows that hold a target (more candidates, more detections) spread over all waves
+    const int f = tile % nf;
+    const int lt = tile / nf;                    // wave tile within the frame
+    const int r0 = lt * WR;
     const float* src = map + ((size_t)f * ns + r0) * NC;
 #pragma unroll
     for (int i = 0; i < WR * NC / 4 / 64; ++i) {
@@ -572,7 +576,8 @@ k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int til
     pass_sync<false>();
     fill_halo<NC, P>(mags + (lane / P) * REGM, lane % P);
     pass_sync<false>();
-    cfar1d_dispatch<NC>(mags, list, lane / P, lane % P, r0, frame0 + f, tile0 + tile, cf, sink);
+    cfar1d_dispatch<NC>(mags, list, lane / P, lane % P, r0, frame0 + f, tile0 + f * tiles_per_frame + lt, cf,
+                        sink);
     pass_sync<false>();  // the region is reused by the next tile
   }
 }
@@ -605,6 +610,7 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
   float2* const wreg = reinterpret_cast<float2*>(mags);
   uint32_t* const list = reinterpret_cast<uint32_t*>(mags + Gm::LIST);
   const int tiles_per_frame = ns / WR;
+  const int nf = n_tiles / tiles_per_frame;
   const int T = 1 << lgT;
   const int lgncb = __builtin_ctz(NC) - lgT;
   // Doppler window for this lane's chirps c = t + P m.  MTI off: K1 already applied it
@@ -624,8 +630,11 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
   for (int tile = blockIdx.x * WPB + wv; tile < n_tiles; tile += gridDim.x * WPB) {
     const int t = opaque(t0);
     float2* buf = wreg + rr * REGD;
-    const int f = tile / tiles_per_frame;
-    const int r0 = (tile - f * tiles_per_frame) * WR;
+    // frame-minor order: consecutive tiles are the same rows of consecutive frames, so the
+    // rows that hold a target (more candidates, more detections) spread over all waves
+    const int f = tile % nf;
+    const int lt = tile / nf;                    // wave tile within the frame
+    const int r0 = lt * WR;
     const int r = r0 + rr;
     const uint32_t rbase = (uint32_t)(r >> lgRB) << lgncb;
     const uint32_t rin = (uint32_t)(r & ((1 << lgRB) - 1));
@@ -716,7 +725,8 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
         }
       }
     }
-    if (cf.enabled) cfar1d_dispatch<NC>(mags, list, rr, t, r0, frame0 + f, tile0 + tile, cf, sink);
+    if (cf.enabled)
+      cfar1d_dispatch<NC>(mags, list, rr, t, r0, frame0 + f, tile0 + f * tiles_per_frame + lt, cf, sink);
     pass_sync<false>();  // the region is reused by the next tile
   }
 }
