@@ -46,6 +46,55 @@ __device__ __forceinline__ int opaque(int x) {
   return x;
 }
 
+// Cache policy of the streamed HBM traffic (build-time switches, measured by tools/ablate.py
+// against variant builds): NT = non-temporal (`nt` on the global load/store).
+#ifndef FMCW_NT_CUBE      // K1 loads of the input cube (read once)
+#define FMCW_NT_CUBE 0
+#endif
+#ifndef FMCW_NT_SPEC_ST   // K1 stores of the corner-turned spectrum (re-read by K2)
+#define FMCW_NT_SPEC_ST 0
+#endif
+#ifndef FMCW_NT_SPEC_LD   // K2 loads of the spectrum (read once)
+#define FMCW_NT_SPEC_LD 0
+#endif
+#ifndef FMCW_NT_MAP       // K2 stores of the range-Doppler map (written once)
+#define FMCW_NT_MAP 0
+#endif
+#ifndef FMCW_K1_TDIV    // K1 chirps per workgroup divided by this (>= 2 chirps kept)
+#define FMCW_K1_TDIV 1
+#endif
+#ifndef FMCW_K1_WAVES   // K1 waves per SIMD requested from the register allocator (0 = none)
+#define FMCW_K1_WAVES 0
+#endif
+typedef float fmcw_f4v __attribute__((ext_vector_type(4)));
+typedef float fmcw_f2v __attribute__((ext_vector_type(2)));
+typedef uint32_t fmcw_u2v __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ float4 ld_f4(const void* p) {
+  fmcw_f4v v;
+  if constexpr (NT) v = __builtin_nontemporal_load(reinterpret_cast<const fmcw_f4v*>(p));
+  else v = *reinterpret_cast<const fmcw_f4v*>(p);
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+template <bool NT>
+__device__ __forceinline__ float2 ld_f2(const void* p) {
+  fmcw_f2v v;
+  if constexpr (NT) v = __builtin_nontemporal_load(reinterpret_cast<const fmcw_f2v*>(p));
+  else v = *reinterpret_cast<const fmcw_f2v*>(p);
+  return make_float2(v.x, v.y);
+}
+template <bool NT>
+__device__ __forceinline__ fmcw_u2v ld_u2(const void* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const fmcw_u2v*>(p));
+  else return *reinterpret_cast<const fmcw_u2v*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void st_f4(void* p, float4 x) {
+  const fmcw_f4v v = {x.x, x.y, x.z, x.w};
+  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<fmcw_f4v*>(p));
+  else *reinterpret_cast<fmcw_f4v*>(p) = v;
+}
+
 // exp(-2 pi i e / LR), 0 <= e < LR, LR a power of two: argument reduced to (-1/2, 1/2] rev.
 template <int LR>
 __device__ __forceinline__ float2 twiddle(int e) {

@@ -91,11 +91,11 @@ namespace {
 using RangeFn = void (*)(const void*, float2*, const float*, const float*, int, int);
 
 template <int N>
-RangeFn range_fn(int dtype) {
+RangeFn range_fn(int dtype, bool q15) {
   switch (dtype) {
     case FMCW_IN_F32: return k_range<N, LoadF32>;
     case FMCW_IN_F16: return k_range<N, LoadF16>;
-    case FMCW_IN_I16: return k_range<N, LoadI16>;
+    case FMCW_IN_I16: return q15 ? k_range<N, LoadI16, true> : k_range<N, LoadI16>;
   }
   return nullptr;
 }
@@ -105,9 +105,10 @@ struct RangeInfo {
   int T, RB, NT;
 };
 
-RangeInfo range_info(uint32_t n, int dtype) {
+RangeInfo range_info(uint32_t n, int dtype, int window = FMCW_WIN_HAMMING) {
+  const bool q15 = window == FMCW_WIN_Q15_RTL;
   switch (n) {
-#define R_(N) case N: return {range_fn<N>(dtype), RangeGeom<N>::T, RangeGeom<N>::RB, RangeGeom<N>::NT};
+#define R_(N) case N: return {range_fn<N>(dtype, q15), RangeGeom<N>::T, RangeGeom<N>::RB, RangeGeom<N>::NT};
     R_(64) R_(128) R_(256) R_(512) R_(1024) R_(2048) R_(4096) R_(8192)
 #undef R_
   }
@@ -210,8 +211,10 @@ int validate(const fmcw_config& c) {
   if (c.n_rx < 1 || c.n_rx > 64) return fail(FMCW_EINVAL, "n_rx=%u: must be in [1, 64]", c.n_rx);
   if (c.in_dtype < FMCW_IN_F32 || c.in_dtype > FMCW_IN_I16)
     return fail(FMCW_EINVAL, "in_dtype=%d unknown", c.in_dtype);
-  if (c.window != FMCW_WIN_NONE && c.window != FMCW_WIN_HAMMING)
+  if (c.window != FMCW_WIN_NONE && c.window != FMCW_WIN_HAMMING && c.window != FMCW_WIN_Q15_RTL)
     return fail(FMCW_EINVAL, "window=%d unknown", c.window);
+  if (c.window == FMCW_WIN_Q15_RTL && c.in_dtype != FMCW_IN_I16)
+    return fail(FMCW_EINVAL, "window Q15_RTL windows int16 ADC words: needs in_dtype I16");
   if (c.mag_mode != FMCW_MAG_ABS && c.mag_mode != FMCW_MAG_AMBM)
     return fail(FMCW_EINVAL, "mag_mode=%d unknown", c.mag_mode);
   if (c.mag_mode == FMCW_MAG_AMBM && c.n_rx != 1)
@@ -249,7 +252,15 @@ int validate(const fmcw_config& c) {
 // (window_multiplier.vhd:34-49, :97-102).  WIN_NONE uploads ones.
 std::vector<float> window_table(uint32_t n, int kind) {
   std::vector<float> w(n, 1.0f);
-  if (kind == FMCW_WIN_HAMMING) {
+  if (kind == FMCW_WIN_Q15_RTL) {  // ROM integers c = integer(w * 32767) (:43-46), mirrored
+    const uint32_t half = n / 2;
+    for (uint32_t i = 0; i < n; ++i) {
+      uint32_t a = i < half ? i : n - 1 - i;
+      if (a > half - 1) a = half - 1;
+      const double wa = 0.54 - 0.46 * std::cos(2.0 * M_PI * (double)a / (double)(n - 1));
+      w[i] = (float)std::min(32767.0, std::floor(wa * 32767.0 + 0.5));
+    }
+  } else if (kind == FMCW_WIN_HAMMING) {
     const uint32_t half = n / 2;
     for (uint32_t i = 0; i < n; ++i) {
       uint32_t a = i < half ? i : n - 1 - i;
@@ -449,7 +460,7 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   h->cfg = *cfg;
   const fmcw_config& c = h->cfg;
   h->n_cu = prop.multiProcessorCount;
-  const RangeInfo ri = range_info(c.n_range, c.in_dtype);
+  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window);
   h->T = ri.T;
   h->RB = ri.RB;
   h->lgT = __builtin_ctz(ri.T);
@@ -502,13 +513,16 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   ALLOC(h->block_sum, ((h->n_wg_max + 1023) / 1024 + 1) * sizeof(uint32_t));
 #undef ALLOC
   {
-    std::vector<float> wr = window_table(c.n_range, c.window), wd = window_table(c.n_doppler, c.window);
+    std::vector<float> wr = window_table(c.n_range, c.window), wd = window_table(c.n_doppler, c.window == FMCW_WIN_Q15_RTL ? FMCW_WIN_HAMMING : c.window);
     if (hipMemcpy(h->win_r, wr.data(), wr.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(h->win_d, wd.data(), wd.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(h->wg_count, 0, h->n_wg_max * sizeof(uint32_t)) != hipSuccess)
       return cleanup(fail(FMCW_EHIP, "window upload failed"));
   }
   occupancy_grid(ri.fn, ri.NT, 0, h->n_cu, &h->grid_range);
+#ifdef FMCW_K1_GRID_PER_CU  // tuning switch (tools/build_variants.sh): K1 workgroups per CU
+  h->grid_range = std::min(h->grid_range, FMCW_K1_GRID_PER_CU * h->n_cu);
+#endif
   const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode);
   occupancy_grid(di.fn, di.NT, 0, h->n_cu, &h->grid_doppler);
   if (c.cfar_kind == FMCW_CFAR_OS2D) {
@@ -549,7 +563,7 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
   if (c.cfar_kind != FMCW_CFAR_NONE && !n_dets_dev)
     return fail(FMCW_EINVAL, "n_dets_dev is required when a CFAR is configured");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const RangeInfo ri = range_info(c.n_range, c.in_dtype);
+  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window);
   const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode);
   const size_t frame_px = (size_t)c.n_range * c.n_doppler;
   const size_t in_frame_bytes = cube_bytes(c, 1);
@@ -660,7 +674,7 @@ int fmcw_range_ct(fmcw_handle* h, const void* cube, size_t n_frames, void* spec,
   const fmcw_config& c = h->cfg;
   if (n_frames < 1 || n_frames > c.max_frames) return fail(FMCW_EINVAL, "n_frames out of range");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const RangeInfo ri = range_info(c.n_range, c.in_dtype);
+  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window);
   const size_t in_frame_bytes = cube_bytes(c, 1);
   const size_t fr_px = (size_t)c.n_rx * c.n_range * c.n_doppler;
   for (size_t f0 = 0; f0 < n_frames; f0 += h->chunk) {

@@ -30,29 +30,37 @@ namespace fmcw {
 struct LoadF32 {
   static constexpr int bytes = 8;
   __device__ __forceinline__ static float4 load2(const void* base, size_t idx) {
-    return *reinterpret_cast<const float4*>(reinterpret_cast<const float2*>(base) + idx);
+    return ld_f4<FMCW_NT_CUBE>(reinterpret_cast<const float2*>(base) + idx);
   }
 };
 struct LoadF16 {
   static constexpr int bytes = 4;
   __device__ __forceinline__ static float4 load2(const void* base, size_t idx) {
     typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-    const h4 h = *reinterpret_cast<const h4*>(reinterpret_cast<const uint32_t*>(base) + idx);
+    const fmcw_u2v u = ld_u2<FMCW_NT_CUBE>(reinterpret_cast<const uint32_t*>(base) + idx);
+    const h4 h = __builtin_bit_cast(h4, u);
     return make_float4((float)h[0], (float)h[1], (float)h[2], (float)h[3]);
   }
 };
 struct LoadI16 {
   static constexpr int bytes = 4;
   __device__ __forceinline__ static float4 load2(const void* base, size_t idx) {
-    const short4 s = *reinterpret_cast<const short4*>(reinterpret_cast<const uint32_t*>(base) + idx);
-    return make_float4((float)s.x, (float)s.y, (float)s.z, (float)s.w);
+    typedef short s4 __attribute__((ext_vector_type(4)));
+    const fmcw_u2v u = ld_u2<FMCW_NT_CUBE>(reinterpret_cast<const uint32_t*>(base) + idx);
+    const s4 s = __builtin_bit_cast(s4, u);
+    return make_float4((float)s[0], (float)s[1], (float)s[2], (float)s[3]);
   }
 };
 
 // K1 geometry per range-FFT size: T chirps per workgroup, RB = 128/T (1 KiB chunks).
 template <int N> struct RangeGeom {
   static constexpr int P = N / 16;                   // threads per transform
-  static constexpr int T = N <= 128 ? 32 : N <= 512 ? 16 : N == 1024 ? 8 : N == 2048 ? 4 : 2;
+  // Measured on MI355X (config 2, tools/ablate.py over build variants): at N = 1024, T = 4
+  // (4 waves, 35 KiB LDS, 3 workgroups per CU at 141 VGPRs) beats T = 8 (8 waves, one
+  // workgroup per CU) by 9 % in K1 with K2 unchanged; T = 2 is 3 % faster again in K1 but
+  // halves K2's read runs (64 B) and costs more there than it saves.
+  static constexpr int T0 = N <= 128 ? 16 : N <= 512 ? 8 : N == 1024 ? 4 : 2;
+  static constexpr int T = T0 / FMCW_K1_TDIV >= 2 ? T0 / FMCW_K1_TDIV : 2;
   static constexpr int NT = T * P;                   // threads per workgroup
   static constexpr int RB = 128 / T;                 // range bins per 1 KiB chunk
   static constexpr int REG = padded(N) + 4;          // LDS row (complex) per chirp
@@ -64,8 +72,12 @@ template <int N> struct RangeGeom {
 // grid-stride over all chirp groups.  Each thread: 8 coalesced 16-B loads, windowing,
 // radix-8 pass in registers, Stockham passes through LDS, then the tiled transposed store.
 // --------------------------------------------------------------------------------------
-template <int N, typename LD>
+// Q15 = RTL-compat integer range window (FMCW_WIN_Q15_RTL, int16 input): `win` then holds the
+// ROM integers c[n] (exact in fp32) and each sample is windowed as sat16((x c + 2^14) >> 14)
+// (window_multiplier.vhd:146-158) before it becomes fp32.
+template <int N, typename LD, bool Q15 = false>
 __global__ void __launch_bounds__(RangeGeom<N>::NT)
+__attribute__((amdgpu_waves_per_eu(FMCW_K1_WAVES > 0 && N < 8192 ? FMCW_K1_WAVES : 1)))
 k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* __restrict__ win,
         const float* __restrict__ chirp_w, int nc, int n_groups) {
   using Gm = RangeGeom<N>;
@@ -76,11 +88,6 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
   const int q = tid / P;  // chirp within the group
   const int t0 = tid % P;
   const int ncb = nc / T;
-
-  // window coefficients for this thread's samples 2t + {0,1} + (N/8) m
-  float2 w[8];
-#pragma unroll
-  for (int m = 0; m < 8; ++m) w[m] = *reinterpret_cast<const float2*>(win + 2 * t0 + (N / 8) * m);
 
   // transposed-store geometry: piece i of this thread is range r0 + i*N/8, chirps c0, c0+1
   const int e0 = 2 * tid;
@@ -107,14 +114,30 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
     // Doppler window of this chirp folded in (K2 then skips it; FFT linearity), or 1
     const float cw = chirp_w ? chirp_w[cb * T + q] : 1.f;
 
+    // window coefficients for samples 2t + {0,1} + (N/8) m, re-read (L1/L2 hits) every group
+    // rather than held: 16 VGPRs fewer across the LDS passes (the register peak)
+    float2 w[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) w[m] = *reinterpret_cast<const float2*>(win + 2 * t + (N / 8) * m);
+
     __syncthreads();  // previous group's transposed reads are done with lds
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       float2 v[8];
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
-        const float we = (e ? w[m].y : w[m].x) * cw;
-        v[m] = e ? make_float2(a[m].z * we, a[m].w * we) : make_float2(a[m].x * we, a[m].y * we);
+        if constexpr (Q15) {
+          const int c = (int)(e ? w[m].y : w[m].x);
+          const float xi = e ? a[m].z : a[m].x, xq = e ? a[m].w : a[m].y;
+          auto win16 = [c](float x) {
+            const int y = ((int)x * c + (1 << 14)) >> 14;  // floor: arithmetic shift
+            return (float)min(max(y, -32768), 32767);
+          };
+          v[m] = make_float2(win16(xi) * cw, win16(xq) * cw);
+        } else {
+          const float we = (e ? w[m].y : w[m].x) * cw;
+          v[m] = e ? make_float2(a[m].z * we, a[m].w * we) : make_float2(a[m].x * we, a[m].y * we);
+        }
       }
       Dft<8>::run(v);
       float2* d = buf + pad16((2 * t + e) * 8);
@@ -149,7 +172,7 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
         v0 = lds[c0 * REG + pad16(r0 + i * (N / 8))];
         v1 = lds[(c0 + 1) * REG + pad16(r0 + i * (N / 8))];
       }
-      *reinterpret_cast<float4*>(dst + i * dstep) = make_float4(v0.x, v0.y, v1.x, v1.y);
+      st_f4<FMCW_NT_SPEC_ST>(dst + i * dstep, make_float4(v0.x, v0.y, v1.x, v1.y));
     }
   }
 }
@@ -646,7 +669,7 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
 
     for (int rx = 0; rx < nrx; ++rx) {
       const float2* src = inter + ((size_t)f * nrx + rx) * (size_t)ns * NC;
-      auto at = [&](uint32_t c) -> float2 { return src[off_of(rbase, rin, c)]; };
+      auto at = [&](uint32_t c) -> float2 { return ld_f2<FMCW_NT_SPEC_LD>(src + off_of(rbase, rin, c)); };
       float2 v[16];
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
@@ -716,7 +739,7 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
         const int e = 4 * (lane + 64 * i);
         const int rl = e / NC, d = e - rl * NC;
         const float4 v = *reinterpret_cast<const float4*>(mags + rl * REGM + midx(d));
-        if (lin_map) *reinterpret_cast<float4*>(lin_map + mbase + e) = v;
+        if (lin_map) st_f4<FMCW_NT_MAP>(lin_map + mbase + e, v);
         if (db_map) {
           const float k = 6.0205999132796239f;  // 20 / log2(10)
           *reinterpret_cast<float4*>(db_map + mbase + e) =

@@ -18,7 +18,7 @@ HEADER_PATH = PKG_ROOT.parent / "include" / "fmcw.h"
 # enums (fmcw.h)
 FMCW_OK, FMCW_EINVAL, FMCW_ENOMEM, FMCW_EHIP, FMCW_EDETCAP, FMCW_ENODEV = 0, -1, -2, -3, -4, -5
 IN_F32, IN_F16, IN_I16 = 0, 1, 2
-WIN_NONE, WIN_HAMMING = 0, 1
+WIN_NONE, WIN_HAMMING, WIN_Q15_RTL = 0, 1, 2
 MAG_ABS, MAG_AMBM = 0, 1
 MAP_LINEAR, MAP_DB = 1, 2
 CFAR_NONE, CFAR_OS1D, CFAR_OS2D = 0, 1, 2

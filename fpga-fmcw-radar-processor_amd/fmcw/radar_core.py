@@ -143,7 +143,7 @@ class RadarCore:
         cfg.mti_mode = L.MTI_OFF if mti_bypass else {2: L.MTI_2PULSE, 3: L.MTI_3PULSE}[NOTCH_MODE]
         cfg.n_range, cfg.n_doppler, cfg.n_rx = N_RANGE, N_DOPPLER, N_RX
         cfg.in_dtype = _IN_DTYPES[in_dtype][0]
-        cfg.window = {"hamming": L.WIN_HAMMING, "none": L.WIN_NONE}[window]
+        cfg.window = {"hamming": L.WIN_HAMMING, "none": L.WIN_NONE, "q15_rtl": L.WIN_Q15_RTL}[window]
         cfg.mag_mode = {"abs": L.MAG_ABS, "ambm": L.MAG_AMBM}[magnitude]
         cfg.map_kind = {"linear": L.MAP_LINEAR, "db": L.MAP_DB}[map_kind]
         cfg.cfar_kind = {"none": L.CFAR_NONE, "os1d": L.CFAR_OS1D, "os2d": L.CFAR_OS2D}[cfar]

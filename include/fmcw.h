@@ -62,7 +62,13 @@ typedef enum {
 } fmcw_status;
 
 typedef enum { FMCW_IN_F32 = 0, FMCW_IN_F16 = 1, FMCW_IN_I16 = 2 } fmcw_in_dtype;
-typedef enum { FMCW_WIN_NONE = 0, FMCW_WIN_HAMMING = 1 } fmcw_window;
+/* FMCW_WIN_Q15_RTL (RTL-compat, in_dtype I16 only): the range window in the RTL's integer
+ * arithmetic, y = sat16((x * c[n] + 2^14) >> 14) with the ROM c = round(32767 w) on the
+ * mirrored half address (window_multiplier.vhd:43-46, :97-102, :146-158) -- a 2x gain with a
+ * +1 LSB bias, so a zero word windows to 1.  The FFTs stay unscaled fp32 and the Doppler window
+ * is the fp32 Hamming table (the reference's second window_multiplier sees the IP's block-
+ * floating-point output, which the build does not reproduce). */
+typedef enum { FMCW_WIN_NONE = 0, FMCW_WIN_HAMMING = 1, FMCW_WIN_Q15_RTL = 2 } fmcw_window;
 /* FMCW_MAG_ABS: |X| = sqrt(re^2 + im^2) (with n_rx > 1: sqrt(sum_rx |X_rx|^2), NCI).
  * FMCW_MAG_AMBM: max(|re|,|im|) + floor(min/4) + floor(min/8) (magnitude_calc.vhd:78-81). */
 typedef enum { FMCW_MAG_ABS = 0, FMCW_MAG_AMBM = 1 } fmcw_mag_mode;

@@ -88,6 +88,14 @@ def window_q15_rtl(x: np.ndarray, n: int) -> np.ndarray:
     return np.clip(y, -32768, 32767).astype(np.int64)
 
 
+def window_q15_cube(cube_i16: np.ndarray) -> np.ndarray:
+    """RTL-compat windowed ADC words of a cube [..., chirp, sample, 2] (I, Q int16) as complex
+    integers: window_q15_rtl on I and on Q (both lanes of window_multiplier.vhd:146-158)."""
+    x = np.asarray(cube_i16)
+    ns = x.shape[-2]
+    return window_q15_rtl(x[..., 0], ns) + 1j * window_q15_rtl(x[..., 1], ns)
+
+
 # ---------------------------------------------------------------------------
 # FFT stages (fp64 reference; unscaled forward DFT, natural order)
 # ---------------------------------------------------------------------------
@@ -337,18 +345,28 @@ def detections(det: np.ndarray, mag: np.ndarray, thr: np.ndarray, frame: int = 0
 # ---------------------------------------------------------------------------
 
 
-def process(cube: np.ndarray, cfar=None, window: bool = True, mti_mode: int = 0):
+def process(cube: np.ndarray, cfar=None, window: bool = True, mti_mode: int = 0,
+            q15_rtl: bool = False):
     """Full hot path for one frame.
 
     cube: [rx, chirp, sample] (or [chirp, sample]) complex.  Returns dict with the
     fp64 map 'mag' [range, doppler], the float32 map used by the CFAR, the
     detection mask and the detection list.  With several rx channels the map is
     the non-coherent integration sqrt(sum_rx |X|^2).
+    q15_rtl: cube is int16 [rx, chirp, sample, 2] and the range window is the RTL's integer
+    Q15 arithmetic (window_q15_cube); the Doppler window stays the fp32 table.
     """
-    c = np.asarray(cube)
-    if c.ndim == 2:
-        c = c[None]
-    rd = doppler_fft(mti(range_ct(c, window), mti_mode), window)  # [rx, range, doppler]
+    if q15_rtl:
+        c = window_q15_cube(cube)
+        if c.ndim == 2:
+            c = c[None]
+        spec = range_ct(c, window=False)
+    else:
+        c = np.asarray(cube)
+        if c.ndim == 2:
+            c = c[None]
+        spec = range_ct(c, window)
+    rd = doppler_fft(mti(spec, mti_mode), window)  # [rx, range, doppler]
     mag = magnitude(rd, rx_axis=0)
     mag32 = mag.astype(np.float32)
     if cfar is None:

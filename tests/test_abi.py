@@ -66,7 +66,8 @@ def test_defaults_mirror_radar_core(lib_built):
     ("n_doppler", 16, b"n_doppler"), ("n_rx", 0, b"n_rx"),
     ("in_dtype", 7, b"in_dtype"), ("map_kind", 0, b"map_kind"),
     ("cfar_kind", 9, b"cfar_kind"), ("cfar2d_scale_override", 8, b"scale_override"),
-    ("mti_mode", 1, b"mti_mode"),
+    ("mti_mode", 1, b"mti_mode"), ("window", 3, b"window"),
+    ("window", 2, b"in_dtype I16"),         # Q15_RTL windows int16 words only (default in f32)
     ("cfar2d_ref_doppler", 12, b"2-D CFAR"), ("max_frames", 0, b"max_frames"),
 ])
 def test_create_rejects_bad_config(lib_built, field, value, msg):

@@ -115,6 +115,33 @@ def test_range_ct_parity(gpu, ns, nc, nrx, dtype, nf):
             assert rel_err(got[f, rx], ref[f, rx]) <= MAP_TOL
 
 
+@pytest.mark.parametrize("ns,nc", [(1024, 128), (256, 32), (4096, 32)])
+def test_range_ct_q15_rtl(gpu, ns, nc):
+    """RTL-compat integer window (FMCW_WIN_Q15_RTL) on full-range int16 words, saturation
+    included, vs the oracle's window_q15_rtl (pinned to the ROM fixture) + fp64 FFT."""
+    rng = np.random.default_rng(ns)
+    cube = rng.integers(-32768, 32768, (2, 1, nc, ns, 2)).astype(np.int16)
+    cube[0, 0, 0, :, :] = -32768                      # saturates low: -32768 * c >> 14 < -32768
+    cube[0, 0, 1, :, :] = 32767
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, in_dtype="i16", window="q15_rtl", cfar="none",
+                   max_frames=2) as core:
+        got = run_range_ct(core, cube, 2)
+    ref = O.range_ct(O.window_q15_cube(cube), window=False)
+    for f in range(2):
+        assert rel_err(got[f, 0], ref[f, 0]) <= MAP_TOL
+
+
+def test_q15_rtl_zero_word_bias(gpu):
+    """The RTL's +1 LSB bias: an all-zero cube windows to 1 + 1j per sample, so every chirp's
+    range spectrum is N (1 + 1j) at bin 0 and zero elsewhere (window_multiplier.vhd:146-149)."""
+    ns, nc = 256, 32
+    cube = np.zeros((1, 1, nc, ns, 2), np.int16)
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, in_dtype="i16", window="q15_rtl", cfar="none") as core:
+        got = run_range_ct(core, cube, 1)[0, 0]         # [range][chirp]
+    np.testing.assert_allclose(got[0], np.full(nc, ns * (1 + 1j)), rtol=1e-6)
+    assert np.abs(got[1:]).max() <= 1e-3
+
+
 def test_window_on_gpu_matches_rom(gpu):
     """Impulse at sample n0 -> |X[r]| = w[n0] for every r, so the GPU's window can be read
     back and held to tb_window_multiplier.vhd:182-240 (DC endpoint/centre, zero, symmetry)."""
@@ -133,7 +160,7 @@ def test_window_on_gpu_matches_rom(gpu):
 
 @pytest.mark.parametrize("case", ["c2_os1d", "c2_os2d", "c3_nci", "ref_core_i16", "small_32",
                                   "min_64x32_os1d", "min_64x32_os2d", "nc1024_os1d",
-                                  "mti2_os2d", "mti3_os1d"])
+                                  "mti2_os2d", "mti3_os1d", "q15_rtl_os2d", "q15_rtl_os1d"])
 def test_process_parity(gpu, case):
     """Full path (map + detections) vs the oracle."""
     cfgs = {
@@ -149,19 +176,25 @@ def test_process_parity(gpu, case):
         # MTI (doppler_notch, radar_core.vhd:329-338) enabled: the next row of SURVEY.md 8f
         "mti2_os2d": dict(ns=1024, nc=128, nrx=1, dtype="i16", cfar="os2d", nf=2, recipe="random_target", mti=2),
         "mti3_os1d": dict(ns=512, nc=64, nrx=2, dtype="f32", cfar="os1d", nf=2, recipe="two_targets", mti=3),
+        # RTL-compat integer range window (window_multiplier.vhd:146-158): SURVEY.md 8f row 2
+        "q15_rtl_os2d": dict(ns=1024, nc=128, nrx=1, dtype="i16", cfar="os2d", nf=2, recipe="random_target",
+                             window="q15_rtl"),
+        "q15_rtl_os1d": dict(ns=1024, nc=256, nrx=1, dtype="i16", cfar="os1d", nf=2, recipe="two_targets",
+                             window="q15_rtl"),
     }
     k = cfgs[case]
     mti = k.get("mti", 0)
     cube = synth.frames(k["nf"], k["ns"], k["nc"], k["nrx"], k["recipe"], dtype=k["dtype"])
     with RadarCore(N_RANGE=k["ns"], N_DOPPLER=k["nc"], N_RX=k["nrx"], in_dtype=k["dtype"],
                    cfar=k["cfar"], max_frames=k["nf"], mti_bypass=(mti == 0),
-                   NOTCH_MODE=mti or 2) as core:
+                   NOTCH_MODE=mti or 2, window=k.get("window", "hamming")) as core:
         out = core.process(cube)
         # stage exactness: the GPU CFAR on its own map == oracle CFAR on that map
         exact = run_cfar_stage(core, out.rd_map)
     cf = O.Cfar1D() if k["cfar"] == "os1d" else O.Cfar2D()
-    ref_mag = np.stack([O.process(to_complex(cube[f], k["dtype"]), None, mti_mode=mti)["mag"]
-                        for f in range(k["nf"])])
+    q15 = k.get("window") == "q15_rtl"
+    ref_mag = np.stack([O.process(cube[f] if q15 else to_complex(cube[f], k["dtype"]), None, mti_mode=mti,
+                                  q15_rtl=q15)["mag"] for f in range(k["nf"])])
     check_map(out.rd_map, ref_mag)
     want = oracle_dets(out.rd_map, cf)
     np.testing.assert_array_equal(out.dets, want)        # fused path, bit-exact

@@ -23,10 +23,16 @@ for s in "$@"; do
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
     tests_all) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 600 python bench.py --steps 10 --warmup 3 ;;
+    bench_c*) run "$s" 600 python bench.py --workload "${s#bench_}" --steps 10 --warmup 3 --no-cpu-baseline ;;
     prof) run rocprof_stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     ablate) run ablate 600 python tools/ablate.py ${ABLATE_ARGS:-} ;;
+    ablate_libs)  # every variant build (tools/build_variants.sh), same ablation variants
+      for lib in fpga-fmcw-radar-processor_amd/lib/var_*.so; do
+        v=$(basename "$lib" .so)
+        FMCW_LIB="$PWD/$lib" run "ablib_${v#var_}" 300 python tools/ablate.py ${ABLATE_ARGS:-}
+      done ;;
     counters) run counters 120 rocprofv3 -L ;;
     pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_LDS_BANK_CONFLICT -d "$OUT/pmc_sq" -o run --output-format csv -- python3 tools/ablate.py --frames 256 --steps 2 --variants base ;;
     pmc_var_*) v=${s#pmc_var_}; run "pmc_$v" 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/pmc_$v" -o run --output-format csv -- python3 tools/ablate.py --frames 256 --steps 2 --variants "$v" ;;

@@ -10,7 +10,7 @@ from pathlib import Path
 
 PKG = Path(__file__).resolve().parent.parent / "fpga-fmcw-radar-processor_amd"
 cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-fvisibility=hidden",
-       "--cuda-device-only", "-c", "-o", "/tmp/fmcw_res.o", str(PKG / "csrc" / "fmcw_api.hip"),
+       *sys.argv[2:], "--cuda-device-only", "-c", "-o", "/tmp/fmcw_res.o", str(PKG / "csrc" / "fmcw_api.hip"),
        "-Rpass-analysis=kernel-resource-usage"]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
 rows, cur = [], None
