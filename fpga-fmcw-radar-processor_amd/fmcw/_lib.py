@@ -51,6 +51,18 @@ class FmcwDet(C.Structure):
                 ("mag", C.c_float), ("threshold", C.c_float)]
 
 
+class FmcwTwsConfig(C.Structure):
+    _fields_ = [("max_tracks", C.c_uint32), ("max_dets", C.c_uint32), ("init_hits", C.c_uint32),
+                ("coast_max", C.c_uint32), ("gate_r", C.c_uint32), ("gate_d", C.c_uint32),
+                ("alpha_q8", C.c_uint32), ("beta_q8", C.c_uint32), ("rtl_compat", C.c_int32)]
+
+
+class FmcwTrack(C.Structure):
+    _fields_ = [("id", C.c_uint16), ("status", C.c_uint8), ("quality", C.c_uint8),
+                ("range_q2", C.c_int32), ("doppler_q2", C.c_int32), ("vel_r", C.c_int32),
+                ("vel_d", C.c_int32), ("last_mag", C.c_uint32), ("age", C.c_uint32)]
+
+
 # every symbol include/fmcw.h declares, with its ctypes signature
 _VP, _SZ, _I, _U32P = C.c_void_p, C.c_size_t, C.c_int, C.POINTER(C.c_uint32)
 SIGNATURES = {
@@ -72,6 +84,10 @@ SIGNATURES = {
     "fmcw_device_free": (_I, [_VP]),
     "fmcw_memcpy": (_I, [_VP, _VP, _SZ, _I]),
     "fmcw_device_count": (_I, [C.POINTER(_I)]),
+    "fmcw_tws_config_default": (None, [C.POINTER(FmcwTwsConfig)]),
+    "fmcw_tws_create": (_I, [C.POINTER(FmcwTwsConfig), C.POINTER(_VP)]),
+    "fmcw_tws_destroy": (_I, [_VP]),
+    "fmcw_tws_scan": (_I, [_VP, _VP, _SZ, C.POINTER(FmcwTrack), _SZ, C.POINTER(_SZ), _U32P]),
 }
 
 _lib = None

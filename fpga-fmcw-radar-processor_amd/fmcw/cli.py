@@ -13,6 +13,8 @@ INPUT formats (by extension):
 Outputs in --out-dir (names the visualizer searches, model/visualize_radar_targets.py:37-107):
   ADR_detections.txt (or ADR_quick_det.txt with --quick): "r d mag" per detection
   radar_output.txt (with --map-file): "r d 0 0 mag" map of the first frame
+  ADR_tracks.txt (with --tracks): the track-while-scan log, one scan per frame
+                 ("TRK id R= D= Q=" / "SCAN_END ACTIVE=n", tb_radar_core.vhd:163-180)
 """
 from __future__ import annotations
 
@@ -23,6 +25,7 @@ import numpy as np
 
 from . import formats, synth
 from .radar_core import RadarCore, adc_words_to_cube
+from .tracker import TwsTracker
 
 
 def load_cube(path: Path, ns: int, nc: int):
@@ -57,11 +60,14 @@ def main(argv=None):
     ap.add_argument("--quick", action="store_true", help="write ADR_quick_det.txt (128x32 geometry)")
     ap.add_argument("--map-file", default=None)
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--tracks", action="store_true", help="run the TWS tracker, write ADR_tracks.txt")
+    ap.add_argument("--tracker-rtl", action="store_true", help="tracker in RTL-compat mode")
+    ap.add_argument("--window", default="hamming", choices=["hamming", "none", "q15_rtl"])
     a = ap.parse_args(argv)
     cube, dt = load_cube(a.input, a.n_range, a.n_doppler)
     nf = cube.shape[0]
     with RadarCore(N_RANGE=a.n_range, N_DOPPLER=a.n_doppler, N_RX=cube.shape[1], in_dtype=dt,
-                   cfar=a.cfar, max_frames=nf, device=a.device) as core:
+                   cfar=a.cfar, max_frames=nf, device=a.device, window=a.window) as core:
         out = core.process(np.ascontiguousarray(cube))
     a.out_dir.mkdir(parents=True, exist_ok=True)
     det_name = "ADR_quick_det.txt" if a.quick else "ADR_detections.txt"
@@ -69,6 +75,13 @@ def main(argv=None):
     if a.map_file:
         formats.write_rd_map(a.out_dir / a.map_file, out.rd_map[0])
     print(f"{nf} frame(s) {a.n_doppler}x{a.n_range}: {n} detections -> {a.out_dir / det_name}")
+    if a.tracks:
+        with TwsTracker(rtl_compat=a.tracker_rtl) as trk:
+            hist = []
+            for f in range(nf):
+                tracks = trk.scan(out.dets[out.dets["frame"] == f])
+                hist.append((tracks, trk.active_tracks))
+        formats.write_tracks(a.out_dir / "ADR_tracks.txt", hist)
 
 
 if __name__ == "__main__":

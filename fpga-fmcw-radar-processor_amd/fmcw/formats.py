@@ -60,3 +60,34 @@ def read_adc_pairs(path) -> np.ndarray:
 
 def write_adc_pairs(path, iq: np.ndarray) -> None:
     np.savetxt(path, np.asarray(iq, np.int64).reshape(-1, 2), fmt="%d")
+
+
+def write_tracks(path, scans) -> None:
+    """Track log as rtl/src/tb_radar_core.vhd:163-180 writes it: per scan, one
+    'TRK id R=range D=doppler Q=quality' line per reported track (R, D = the Q2 trk_range /
+    trk_doppler words as signed integers), then 'SCAN_END ACTIVE=n'.  scans: iterable of
+    (tracks, active) with tracks in fmcw.tracker.TRACK_DTYPE."""
+    with open(path, "w") as f:
+        for tracks, active in scans:
+            for t in tracks:
+                f.write(f"TRK {int(t['id'])} R={int(t['range_q2'])} D={int(t['doppler_q2'])} "
+                        f"Q={int(t['quality'])}\n")
+            f.write(f"SCAN_END ACTIVE={int(active)}\n")
+
+
+def read_tracks(path):
+    """Parse like load_tracks() (model/visualize_radar_targets.py:124-166): returns
+    ({id: [(scan, R, D, Q), ...]}, [active per scan])."""
+    tracks, counts, scan = {}, [], 0
+    for line in Path(path).read_text().splitlines():
+        p = line.split()
+        if not p:
+            continue
+        if p[0] == "TRK":
+            q = next((int(x.split("=")[1]) for x in p[4:] if x.startswith("Q=")), 0)
+            tracks.setdefault(int(p[1]), []).append(
+                (scan, int(p[2].split("=")[1]), int(p[3].split("=")[1]), q))
+        elif p[0] == "SCAN_END":
+            counts.append(int(p[1].split("=")[1]))
+            scan += 1
+    return tracks, counts

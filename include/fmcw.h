@@ -183,6 +183,43 @@ int fmcw_device_free(void* ptr);
 int fmcw_memcpy(void* dst, const void* src, size_t bytes, int kind /*0 H2D,1 D2H,2 D2D*/);
 int fmcw_device_count(int* n);
 
+/* ---- Track-while-scan tracker (host side) ----------------------------------------------
+ * Replaces rtl/src/tws_tracker.vhd (radar_core.vhd:424-438): MAX_TRACKS alpha-beta tracks in
+ * Q2 bins with Q8 gains over the detection list, one scan (= one frame's detections) per
+ * fmcw_tws_scan.  CPU code: serial, <= 64 detections x 64 tracks per scan.
+ * rtl_compat = 1 is the VHDL bit for bit (wrapping field widths, the signal read of
+ * best_distance in ASSOCIATE, the 6-bit detection counter); 0 is the intended tracker (wide
+ * integers, nearest-neighbour association).  Output: firm and coasting tracks in track-file
+ * order, as ST_OUTPUT streams them (:273-295); *n_out = their count (FMCW_EDETCAP if > cap). */
+typedef struct fmcw_tws fmcw_tws;
+typedef struct {
+  uint32_t max_tracks;   /* MAX_TRACKS (32), <= 64 */
+  uint32_t max_dets;     /* detections kept per scan (64, the RTL's MAX_DETS), <= 64 */
+  uint32_t init_hits;    /* INIT_HITS (2) */
+  uint32_t coast_max;    /* COAST_MAX (5) */
+  uint32_t gate_r;       /* ASSOC_GATE_R (10 range bins) */
+  uint32_t gate_d;       /* ASSOC_GATE_D (5 Doppler bins) */
+  uint32_t alpha_q8;     /* ALPHA_GAIN (128 = 0.5), < 256 */
+  uint32_t beta_q8;      /* BETA_GAIN (64 = 0.25), < 256 */
+  int32_t rtl_compat;
+} fmcw_tws_config;
+typedef struct {
+  uint16_t id;           /* trk_id: track-file slot */
+  uint8_t status;        /* trk_status: 2 FIRM, 3 COAST */
+  uint8_t quality;       /* trk_quality 0..15 */
+  int32_t range_q2;      /* trk_range: range bin x 4 */
+  int32_t doppler_q2;    /* trk_doppler: Doppler bin x 4 */
+  int32_t vel_r;         /* trk_vel_r: Q2 range bins per scan */
+  int32_t vel_d;         /* trk_vel_d */
+  uint32_t last_mag;     /* last associated detection magnitude (rounded) */
+  uint32_t age;          /* scans since initiation */
+} fmcw_track;
+void fmcw_tws_config_default(fmcw_tws_config* cfg);
+int fmcw_tws_create(const fmcw_tws_config* cfg, fmcw_tws** out);
+int fmcw_tws_destroy(fmcw_tws* t);
+int fmcw_tws_scan(fmcw_tws* t, const fmcw_det* dets, size_t n_dets, fmcw_track* out, size_t cap,
+                  size_t* n_out, uint32_t* n_active);
+
 #if defined(__GNUC__)
 #pragma GCC visibility pop
 #endif

@@ -9,7 +9,7 @@ pids=()
 for spec in "$@"; do
   name=${spec%%=*}
   defs=${spec#*=}
-  /opt/rocm/bin/hipcc $FLAGS ${defs//,/ } -shared -o "lib/var_${name}.so" csrc/fmcw_api.hip &
+  /opt/rocm/bin/hipcc $FLAGS ${defs//,/ } -shared -o "lib/var_${name}.so" csrc/fmcw_api.hip csrc/tws_tracker.cpp &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait "$p"; done
