@@ -290,6 +290,13 @@ struct Cfar1DArgs {
 // aligned (one ds_read_b128 per 4 cells) and 16 lanes reading blocks 16 cells apart touch 16
 // disjoint bank quads (20 t mod 64 are distinct).
 // --------------------------------------------------------------------------------------
+// |X| from |X|^2: the hardware square root (v_sqrt_f32, <= 1 ulp) instead of the correctly
+// rounded libm sequence (~15 VALU instructions each: denormal scaling plus two fma fix-ups).
+// Magnitudes are specified to 1e-4 relative (BASELINE north_star), the CFAR is exact on
+// whatever map is produced, and |X|^2 is never denormal-sensitive at these scales.  Scaling
+// the input by 2 still scales the map by exactly 2 (an even exponent shift).
+__device__ __forceinline__ float mag_sqrt(float p) { return __builtin_amdgcn_sqrtf(p); }
+
 constexpr int MH = 16;  // halo cells per side
 __host__ __device__ constexpr int midx(int d) { return (d + MH) + (((d + MH) >> 4) << 2); }
 // midx(x + o) - midx(x) for x % 16 == 0 and a compile-time o >= -MH
@@ -427,14 +434,16 @@ __device__ __forceinline__ void cfar1d_wave(const float* mags, uint32_t* list, i
   const float* mrow = mags + rr * RS;
   const int d0 = t * CELLS;
   const int nref = 2 * cf.ref;
+  const int lane = (int)(threadIdx.x & 63);
   uint32_t bits = 0;
+  int total = 0;  // detections of the wave tile (uniform), their cells in list[0, total)
   if constexpr (REF > 0) {
     // Screen, then count exactly where needed.  A group of 4 consecutive reference cells
     // whose minimum satisfies fl(alpha*min) >= cut has all 4 refs at or above cut/alpha
     // (fl(alpha*x) is monotone in x), so 4 * #{such groups} is a lower bound on
     // #{refs : fl(alpha*ref) >= cut}; once it reaches need = n_ref - rank the cell cannot
-    // detect.  The exact count (16 compares) runs only for the cell indices where some lane
-    // of the wave survived (a uniform branch) and decides exactly as the unscreened count.
+    // detect.  The exact count (16 compares) runs only for the survivors (below) and decides
+    // exactly as the unscreened count.
     static_assert(REF % 4 == 0, "reference runs split into groups of 4");
     constexpr int H = REF + GUARD;
     static_assert(H <= MH, "the window stays inside the row halos");
@@ -481,15 +490,44 @@ __device__ __forceinline__ void cfar1d_wave(const float* mags, uint32_t* list, i
             ng += (cf.alpha * g[i + 4 * q] >= cut) + (cf.alpha * g[i + RO + 4 * q] >= cut);
           surv = 4 * ng < need;
         }
-        if (__any(surv)) {
-          const uint32_t cbits = __float_as_uint(cut);
+        bits |= (surv ? 1u : 0u) << (hh * HC + i);
+      }
+    }
+    // Exact count for the survivors only, one survivor per lane.  About 12 of a tile's 1024
+    // cells survive the screen on noise + targets, but they sit in ~8 of the 16 cell
+    // indices, so counting per index for the whole wave (where any lane survived) cost 8 x 16
+    // compares per lane; the ordered survivor list costs one 16-compare round per 64.
+    int n_surv;
+    const int sx = wave_excl_scan(__popc(bits), n_surv);
+    if (n_surv != 0) {  // uniform
+      {
+        int o = sx;
+        for (uint32_t m = bits; m; m &= m - 1, ++o) list[o] = ((uint32_t)rr << 16) | (uint32_t)(d0 + __builtin_ctz(m));
+      }
+      pass_sync<false>();
+      for (int i0 = 0; i0 < n_surv; i0 += 64) {
+        const int i = i0 + lane;
+        bool det = false;
+        uint32_t cell = 0;
+        if (i < n_surv) {
+          cell = list[i];
+          const float* row = mags + (int)(cell >> 16) * RS;
+          const int d = (int)(cell & 0xffffu);
+          const uint32_t cbits = __float_as_uint(row[midx(d)]);
           uint32_t lt = 0;
 #pragma unroll
           for (int j = 0; j < REF; ++j)
-            lt += lt_bit(__float_as_uint(cf.alpha * w[i + j]), cbits) +
-                  lt_bit(__float_as_uint(cf.alpha * w[i + RO + j]), cbits);
-          bits |= ((int)lt > cf.rank ? 1u : 0u) << (hh * HC + i);
+            lt += lt_bit(__float_as_uint(cf.alpha * row[midx(d - GUARD - 1 - j)]), cbits) +
+                  lt_bit(__float_as_uint(cf.alpha * row[midx(d + GUARD + 1 + j)]), cbits);
+          det = (int)lt > cf.rank;
         }
+        // in-place ordered compaction: every lane has read its entry of this round, and the
+        // detections land at positions <= their survivor index
+        const uint64_t bal = __ballot(det);
+        const int pos = total + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        if (det) list[pos] = cell;
+        total += (int)__popcll(bal);
       }
     }
   } else {
@@ -504,20 +542,17 @@ __device__ __forceinline__ void cfar1d_wave(const float* mags, uint32_t* list, i
       }
       bits |= ((int)lt > cf.rank ? 1u : 0u) << i;
     }
-  }
-  int total;
-  const int excl = wave_excl_scan(__popc(bits), total);
-  const uint32_t base = det_reserve_wave(sink, tile, total);
-  if (total == 0) return;  // uniform
-  // Detections cluster (a target lights up consecutive cells of one lane), so the ranked
-  // value is computed one detection per lane over the whole wave, from an ordered list of
-  // cells (rr << 16 | d) in `list` (capacity: the tile's cells).
-  {
+    const int excl = wave_excl_scan(__popc(bits), total);
     int o = excl;
     for (uint32_t m = bits; m; m &= m - 1, ++o) list[o] = ((uint32_t)rr << 16) | (uint32_t)(d0 + __builtin_ctz(m));
   }
+  const uint32_t base = det_reserve_wave(sink, tile, total);
+  if (total == 0) return;  // uniform
+  // Detections cluster (a target lights up consecutive cells of one lane), so the ranked
+  // value is computed one detection per lane over the whole wave, from the ordered list of
+  // detected cells (rr << 16 | d) in `list` (capacity: the tile's cells).
   pass_sync<false>();
-  for (int i = (int)(threadIdx.x & 63); i < total; i += 64) {
+  for (int i = lane; i < total; i += 64) {
     const uint32_t cell = list[i];
     const int rl = (int)(cell >> 16), d = (int)(cell & 0xffffu);
     const float* row = mags + rl * RS;
@@ -614,8 +649,18 @@ k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int til
 // after the canceller (MTI on); the last pass stays in registers and feeds |X|^2 (summed over
 // rx: NCI) directly.
 // --------------------------------------------------------------------------------------
+#ifndef FMCW_K2_PREFETCH  // K2 (MTI off) loads the next (tile, rx) unit while it works on this one
+#define FMCW_K2_PREFETCH 0
+#endif
+#ifndef FMCW_K2_WAVES     // K2 waves per SIMD asked of the register allocator (0 = by geometry)
+#define FMCW_K2_WAVES 0
+#endif
 template <int NC, int MTI>
-__global__ void __launch_bounds__(DopplerGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(MTI == 0 && NC <= 256 ? 3 : 2)))
+constexpr int k2_waves() {
+  return FMCW_K2_WAVES > 0 ? FMCW_K2_WAVES : (MTI == 0 && NC <= 256 && !FMCW_K2_PREFETCH) ? 3 : 2;
+}
+template <int NC, int MTI>
+__global__ void __launch_bounds__(DopplerGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(k2_waves<NC, MTI>())))
 k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int ns, int nrx,
           int lgT, int lgRB, int n_tiles, int frame0, int tile0, float* __restrict__ lin_map,
           float* __restrict__ db_map, int mag_mode, Cfar1DArgs cf, DetSink sink) {
@@ -650,7 +695,35 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
     return ((((rbase + (c >> lgT)) << lgRB) + rin) << lgT) | (c & (uint32_t)(T - 1));
   };
 
-  for (int tile = blockIdx.x * WPB + wv; tile < n_tiles; tile += gridDim.x * WPB) {
+  // Software pipeline (MTI off): the 16 points of the next (tile, rx) unit are loaded into
+  // registers right after this unit's first pass has consumed its own, so a wave keeps 8 KiB
+  // of HBM reads in flight through its FFT, magnitude, map store and CFAR phases instead of
+  // exposing the full load latency once per unit.
+  constexpr bool PF = MTI == 0 && NC <= 256 && FMCW_K2_PREFETCH;
+  const int tile_step = gridDim.x * WPB;
+  auto unit_src = [&](int tl, int rx) -> const float2* {
+    const int fu = tl % nf;
+    const int ru = (tl / nf) * WR + rr;
+    return inter + ((size_t)fu * nrx + rx) * (size_t)ns * NC +
+           off_of((uint32_t)(ru >> lgRB) << lgncb, (uint32_t)(ru & ((1 << lgRB) - 1)), 0);
+  };
+  float2 nxt[PF ? 16 : 1];
+  auto prefetch = [&](int tl, int rx) {
+    if constexpr (PF) {
+      if (tl < n_tiles) {
+        const float2* p = unit_src(tl, rx);
+        const int tq = opaque(t0);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+          const uint32_t c = (uint32_t)(tq + P * m);
+          nxt[m] = ld_f2<FMCW_NT_SPEC_LD>(p + ((((c >> lgT) << lgRB) << lgT) | (c & (uint32_t)(T - 1))));
+        }
+      }
+    }
+  };
+  prefetch(blockIdx.x * WPB + wv, 0);
+
+  for (int tile = blockIdx.x * WPB + wv; tile < n_tiles; tile += tile_step) {
     const int t = opaque(t0);
     float2* buf = wreg + rr * REGD;
     // frame-minor order: consecutive tiles are the same rows of consecutive frames, so the
@@ -674,7 +747,7 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int c = t + P * m;
-        float2 x = at((uint32_t)c);
+        float2 x = PF ? nxt[m] : at((uint32_t)c);
         if constexpr (MTI >= 2) {  // MTI canceller along slow time, zero history (doppler_notch.vhd:72-102)
           const float2 x1 = c >= 1 ? at((uint32_t)(c - 1)) : make_float2(0.f, 0.f);
           if constexpr (MTI == 2) {
@@ -694,6 +767,8 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
         for (int m = 0; m < 16; ++m) d[m] = v[m];
       }
       pass_sync<false>();
+      if (rx + 1 < nrx) prefetch(tile, rx + 1);
+      else prefetch(tile + tile_step, 0);
       float2 X[LG][LR];
       stockham_to_regs<NC, 16, P, false>(buf, t, X);
       if (mag_mode == FMCW_MAG_AMBM) {  // uniform: one branch for the whole block
@@ -721,7 +796,7 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
       float* m0 = mrow + midx(t + P * g);
 #pragma unroll
       for (int m = 0; m < LR; ++m)
-        m0[mpadoff(m * (NC / LR))] = ambm ? acc[g][m] : sqrtf(acc[g][m]);
+        m0[mpadoff(m * (NC / LR))] = ambm ? acc[g][m] : mag_sqrt(acc[g][m]);
     }
     pass_sync<false>();
     if (cf.enabled) {
@@ -839,7 +914,7 @@ __global__ void k_magnitude(const float2* __restrict__ iq, float* __restrict__ o
     const float mx = fmaxf(ai, aq), mn = fminf(ai, aq);
     out[i] = mx + floorf(mn * 0.25f) + floorf(mn * 0.125f);
   } else {
-    out[i] = sqrtf(X.x * X.x + X.y * X.y);
+    out[i] = mag_sqrt(X.x * X.x + X.y * X.y);
   }
 }
 
