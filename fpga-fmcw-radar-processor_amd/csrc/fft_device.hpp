@@ -23,11 +23,71 @@
 
 namespace fmcw {
 
+// Complex arithmetic on packed fp32 (VOP3P v_pk_*_f32: one instruction per complex add, two
+// per complex product).  Left to itself the SLP vectorizer pairs components of *different*
+// complex values and then spends v_mov's re-pairing them (about a third of the FFT's VALU
+// instructions); with FMCW_PK_ASM every butterfly operation is one packed instruction on a
+// (re, im) register pair, the -i rotations and the cross terms of the product folded into
+// op_sel / neg modifiers.
+#ifndef FMCW_PK_ASM
+#define FMCW_PK_ASM 1
+#endif
+typedef float fmcw_cf __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ fmcw_cf pk(float2 a) { return fmcw_cf{a.x, a.y}; }
+__device__ __forceinline__ float2 unpk(fmcw_cf a) { return make_float2(a.x, a.y); }
+#if FMCW_PK_ASM
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) {
+  fmcw_cf r;
+  asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(pk(a)), "v"(pk(b)));
+  return unpk(r);
+}
+__device__ __forceinline__ float2 csub(float2 a, float2 b) {
+  fmcw_cf r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(pk(a)), "v"(pk(b)));
+  return unpk(r);
+}
+#ifndef FMCW_PK_CMUL_ASM
+#define FMCW_PK_CMUL_ASM 1
+#endif
+#if defined(FMCW_PK_NOP1) && FMCW_PK_NOP1
+#define FMCW_PK_NOP "s_nop 1\n"
+#else
+#define FMCW_PK_NOP ""
+#endif
+// a * b = (a.x b.x - a.y b.y, a.x b.y + a.y b.x): t = a.x * (b.x, b.y); r = t + (-a.y b.y, a.y b.x)
+#if FMCW_PK_CMUL_ASM
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  fmcw_cf t, r;
+  asm(FMCW_PK_NOP "v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(pk(a)), "v"(pk(b)));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+      : "=v"(r) : "v"(pk(a)), "v"(pk(b)), "v"(t));
+  return unpk(r);
+}
+#else
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+#endif
+// a + (-i) d = (a.x + d.y, a.y - d.x)   and   a - (-i) d = (a.x - d.y, a.y + d.x)
+__device__ __forceinline__ float2 cadd_negi(float2 a, float2 d) {
+  fmcw_cf r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(pk(a)), "v"(pk(d)));
+  return unpk(r);
+}
+__device__ __forceinline__ float2 csub_negi(float2 a, float2 d) {
+  fmcw_cf r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(pk(a)), "v"(pk(d)));
+  return unpk(r);
+}
+#else
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
+__device__ __forceinline__ float2 cadd_negi(float2 a, float2 d) { return make_float2(a.x + d.y, a.y - d.x); }
+__device__ __forceinline__ float2 csub_negi(float2 a, float2 d) { return make_float2(a.x - d.y, a.y + d.x); }
+#endif
 __device__ __forceinline__ float2 mul_negi(float2 a) { return make_float2(a.y, -a.x); }  // -i a
 __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
 
@@ -62,6 +122,9 @@ __device__ __forceinline__ int opaque(int x) {
 #endif
 #ifndef FMCW_K1_TDIV    // K1 chirps per workgroup divided by this (>= 2 chirps kept)
 #define FMCW_K1_TDIV 1
+#endif
+#ifndef FMCW_K1_T        // K1 chirps per workgroup override (0 = by range length)
+#define FMCW_K1_T 0
 #endif
 #ifndef FMCW_K1_WAVES   // K1 waves per SIMD requested from the register allocator (0 = none)
 #define FMCW_K1_WAVES 0
@@ -99,7 +162,15 @@ __device__ __forceinline__ void st_f4(void* p, float4 x) {
 template <int LR>
 __device__ __forceinline__ float2 twiddle(int e) {
   const float rev = (e > LR / 2) ? (float)(LR - e) * (1.0f / LR) : -(float)e * (1.0f / LR);
-  return make_float2(__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev));
+  float c = __builtin_amdgcn_cosf(rev), s = __builtin_amdgcn_sinf(rev);
+#if FMCW_PK_ASM
+  // v_cos/v_sin are transcendental: a VALU reading their result needs wait states, which the
+  // hazard recognizer does not insert ahead of an inline-asm reader (the packed cmul above).
+  // Measured: without this, range transforms with twiddles consumed back to back came out
+  // wrong (N = 4096); two wait states here make every later reader safe.
+  asm volatile("s_nop 1" : "+v"(c), "+v"(s));
+#endif
+  return make_float2(c, s);
 }
 
 // Twiddles of one radix-R group, w^m for w = exp(-2 pi i k / LR), m < R: the powers
@@ -135,11 +206,11 @@ __device__ __forceinline__ void dft2(float2& a, float2& b) {
 
 __device__ __forceinline__ void dft4(float2& x0, float2& x1, float2& x2, float2& x3) {
   const float2 a0 = cadd(x0, x2), a1 = csub(x0, x2);
-  const float2 a2 = cadd(x1, x3), a3 = mul_negi(csub(x1, x3));
+  const float2 a2 = cadd(x1, x3), d = csub(x1, x3);
   x0 = cadd(a0, a2);
   x2 = csub(a0, a2);
-  x1 = cadd(a1, a3);
-  x3 = csub(a1, a3);
+  x1 = cadd_negi(a1, d);   // a1 + (-i) d
+  x3 = csub_negi(a1, d);
 }
 
 template <int R> struct Dft;
@@ -157,12 +228,11 @@ template <> struct Dft<8> {
     dft4(e0, e1, e2, e3);
     dft4(o0, o1, o2, o3);
     const float c = 0.70710678118654752440f;
-    const float2 t1 = make_float2(c * (o1.x + o1.y), c * (o1.y - o1.x));    // w8^1 o1
-    const float2 t2 = mul_negi(o2);                                          // w8^2 o2
-    const float2 t3 = make_float2(c * (o3.y - o3.x), -c * (o3.x + o3.y));   // w8^3 o3
+    const float2 t1 = cscale(cadd_negi(o1, o1), c);     // w8^1 o1 = c (o1.x + o1.y, o1.y - o1.x)
+    const float2 t3 = cscale(csub_negi(o3, o3), -c);    // w8^3 o3 = -c (o3.x - o3.y, o3.y + o3.x)
     v[0] = cadd(e0, o0); v[4] = csub(e0, o0);
     v[1] = cadd(e1, t1); v[5] = csub(e1, t1);
-    v[2] = cadd(e2, t2); v[6] = csub(e2, t2);
+    v[2] = cadd_negi(e2, o2); v[6] = csub_negi(e2, o2);  // w8^2 o2 = -i o2
     v[3] = cadd(e3, t3); v[7] = csub(e3, t3);
   }
 };
@@ -177,17 +247,27 @@ template <> struct Dft<16> {
     const float c16 = 0.92387953251128675613f;  // cos(pi/8)
     const float s16 = 0.38268343236508977173f;  // sin(pi/8)
     // w16^e = (cos(2 pi e/16), -sin(2 pi e/16))
-    v[5] = cmul(v[5], make_float2(c16, -s16));   // n2=1,k1=1: e=1
-    v[9] = cmul(v[9], make_float2(c8, -c8));     // n2=1,k1=2: e=2
-    v[13] = cmul(v[13], make_float2(s16, -c16)); // n2=1,k1=3: e=3
-    v[6] = cmul(v[6], make_float2(c8, -c8));     // n2=2,k1=1: e=2
-    v[10] = mul_negi(v[10]);                     // n2=2,k1=2: e=4
-    v[14] = cmul(v[14], make_float2(-c8, -c8));  // n2=2,k1=3: e=6
-    v[7] = cmul(v[7], make_float2(s16, -c16));   // n2=3,k1=1: e=3
-    v[11] = cmul(v[11], make_float2(-c8, -c8));  // n2=3,k1=2: e=6
-    v[15] = cmul(v[15], make_float2(-c16, s16)); // n2=3,k1=3: e=9
-#pragma unroll
-    for (int k1 = 0; k1 < 4; ++k1) dft4(v[4 * k1], v[4 * k1 + 1], v[4 * k1 + 2], v[4 * k1 + 3]);
+    // w8 = c8 (1 - i), w8^3 = -c8 (1 + i): a packed add with a -i operand and a scale
+    v[5] = cmul(v[5], make_float2(c16, -s16));      // n2=1,k1=1: e=1
+    v[9] = cscale(cadd_negi(v[9], v[9]), c8);       // n2=1,k1=2: e=2
+    v[13] = cmul(v[13], make_float2(s16, -c16));    // n2=1,k1=3: e=3
+    v[6] = cscale(cadd_negi(v[6], v[6]), c8);       // n2=2,k1=1: e=2
+    //                                                 n2=2,k1=2: e=4, -i, folded below
+    v[14] = cscale(csub_negi(v[14], v[14]), -c8);   // n2=2,k1=3: e=6
+    v[7] = cmul(v[7], make_float2(s16, -c16));      // n2=3,k1=1: e=3
+    v[11] = cscale(csub_negi(v[11], v[11]), -c8);   // n2=3,k1=2: e=6
+    v[15] = cmul(v[15], make_float2(-c16, s16));    // n2=3,k1=3: e=9
+    dft4(v[0], v[1], v[2], v[3]);
+    dft4(v[4], v[5], v[6], v[7]);
+    {  // dft4(v[8], v[9], -i v[10], v[11])
+      const float2 a0 = cadd_negi(v[8], v[10]), a1 = csub_negi(v[8], v[10]);
+      const float2 a2 = cadd(v[9], v[11]), d = csub(v[9], v[11]);
+      v[8] = cadd(a0, a2);
+      v[10] = csub(a0, a2);
+      v[9] = cadd_negi(a1, d);
+      v[11] = csub_negi(a1, d);
+    }
+    dft4(v[12], v[13], v[14], v[15]);
     // now v[4 k1 + k2] = X[k1 + 4 k2]; transpose the 4x4 index to natural order
     float2 t[16];
 #pragma unroll

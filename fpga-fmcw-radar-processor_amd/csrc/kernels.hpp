@@ -59,7 +59,7 @@ template <int N> struct RangeGeom {
   // (4 waves, 35 KiB LDS, 3 workgroups per CU at 141 VGPRs) beats T = 8 (8 waves, one
   // workgroup per CU) by 9 % in K1 with K2 unchanged; T = 2 is 3 % faster again in K1 but
   // halves K2's read runs (64 B) and costs more there than it saves.
-  static constexpr int T0 = N <= 128 ? 16 : N <= 512 ? 8 : N == 1024 ? 4 : 2;
+  static constexpr int T0 = FMCW_K1_T > 0 && N == 1024 ? FMCW_K1_T : N <= 128 ? 16 : N <= 512 ? 8 : N == 1024 ? 4 : 2;
   static constexpr int T = T0 / FMCW_K1_TDIV >= 2 ? T0 / FMCW_K1_TDIV : 2;
   static constexpr int NT = T * P;                   // threads per workgroup
   static constexpr int RB = 128 / T;                 // range bins per 1 KiB chunk
@@ -650,7 +650,10 @@ k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int til
 // rx: NCI) directly.
 // --------------------------------------------------------------------------------------
 #ifndef FMCW_K2_PREFETCH  // K2 (MTI off) loads the next (tile, rx) unit while it works on this one
-#define FMCW_K2_PREFETCH 0
+#define FMCW_K2_PREFETCH 1
+#endif
+#ifndef FMCW_K2_ORDER     // K2 tile order (see k_doppler)
+#define FMCW_K2_ORDER 1
 #endif
 #ifndef FMCW_K2_WAVES     // K2 waves per SIMD asked of the register allocator (0 = by geometry)
 #define FMCW_K2_WAVES 0
@@ -700,10 +703,27 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
   // of HBM reads in flight through its FFT, magnitude, map store and CFAR phases instead of
   // exposing the full load latency once per unit.
   constexpr bool PF = MTI == 0 && NC <= 256 && FMCW_K2_PREFETCH;
+  // Tile order.  FMCW_K2_ORDER 0: frame-minor over all waves (tile -> f = tile % nf).
+  // Measured on config 2: order 1 cuts K2 0.905 -> 0.874 us/frame (map-store cost 0.13 -> 0.085).
+  // FMCW_K2_ORDER 1: the WPB waves of a workgroup take WPB consecutive wave tiles (row
+  // groups) of one frame, frame-minor over workgroups, so the 4 x WR rows they read from
+  // each 1 KiB block of the tiled spectrum are requested together (DRAM page locality).
+  const bool grp = FMCW_K2_ORDER != 0 && tiles_per_frame % WPB == 0;
+  auto tile_fl = [&](int tl, int& fo, int& lo) {
+    if (grp) {
+      const int u = tl / WPB;
+      fo = u % nf;
+      lo = (u / nf) * WPB + (tl % WPB);
+    } else {
+      fo = tl % nf;
+      lo = tl / nf;
+    }
+  };
   const int tile_step = gridDim.x * WPB;
   auto unit_src = [&](int tl, int rx) -> const float2* {
-    const int fu = tl % nf;
-    const int ru = (tl / nf) * WR + rr;
+    int fu, lu;
+    tile_fl(tl, fu, lu);
+    const int ru = lu * WR + rr;
     return inter + ((size_t)fu * nrx + rx) * (size_t)ns * NC +
            off_of((uint32_t)(ru >> lgRB) << lgncb, (uint32_t)(ru & ((1 << lgRB) - 1)), 0);
   };
@@ -728,8 +748,8 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
     float2* buf = wreg + rr * REGD;
     // frame-minor order: consecutive tiles are the same rows of consecutive frames, so the
     // rows that hold a target (more candidates, more detections) spread over all waves
-    const int f = tile % nf;
-    const int lt = tile / nf;                    // wave tile within the frame
+    int f, lt;                                   // frame, wave tile within the frame
+    tile_fl(tile, f, lt);
     const int r0 = lt * WR;
     const int r = r0 + rr;
     const uint32_t rbase = (uint32_t)(r >> lgRB) << lgncb;
