@@ -473,24 +473,28 @@ __device__ __forceinline__ void cfar1d_wave(const float* mags, uint32_t* list, i
         for (int k = 0; k < WH - 3; ++k) g[k] = fminf(m2[k], m2[k + 2]);
       }
 #pragma unroll
+      // survivor bits by integer arithmetic on the (non-negative) float patterns: a float
+      // compare would produce one SGPR-pair lane mask per cell and push the kernel into SGPR
+      // spills (v_readlane/v_writelane in the tile loop)
       for (int i = 0; i < HC; ++i) {
-        const float cut = w[H + i];
-        bool surv;
+        const uint32_t cbits = __float_as_uint(w[H + i]);
+        uint32_t sb;
         if (one_group) {
           float M = g[i];
 #pragma unroll
           for (int q = 1; q < NGS; ++q) M = fmaxf(M, g[i + 4 * q]);
 #pragma unroll
           for (int q = 0; q < NGS; ++q) M = fmaxf(M, g[i + RO + 4 * q]);
-          surv = cf.alpha * M < cut;
+          sb = lt_bit(__float_as_uint(cf.alpha * M), cbits);  // alpha M < cut
         } else {
-          int ng = 0;
+          uint32_t nlt = 0;  // groups with alpha * min < cut
 #pragma unroll
           for (int q = 0; q < NGS; ++q)
-            ng += (cf.alpha * g[i + 4 * q] >= cut) + (cf.alpha * g[i + RO + 4 * q] >= cut);
-          surv = 4 * ng < need;
+            nlt += lt_bit(__float_as_uint(cf.alpha * g[i + 4 * q]), cbits) +
+                   lt_bit(__float_as_uint(cf.alpha * g[i + RO + 4 * q]), cbits);
+          sb = 4 * (2 * NGS - (int)nlt) < need ? 1u : 0u;
         }
-        bits |= (surv ? 1u : 0u) << (hh * HC + i);
+        bits |= sb << (hh * HC + i);
       }
     }
     // Exact count for the survivors only, one survivor per lane.  About 12 of a tile's 1024
@@ -511,14 +515,17 @@ __device__ __forceinline__ void cfar1d_wave(const float* mags, uint32_t* list, i
         uint32_t cell = 0;
         if (i < n_surv) {
           cell = list[i];
-          const float* row = mags + (int)(cell >> 16) * RS;
           const int d = (int)(cell & 0xffffu);
-          const uint32_t cbits = __float_as_uint(row[midx(d)]);
+          const float* cp = mags + (int)(cell >> 16) * RS + midx(d);
+          // midx(d + o) - midx(d) = o + 4 floor((q + o) / 16), q = (d + MH) % 16, |o| < 16
+          const int q = (d + MH) & 15;
+          auto ref = [&](int o) { return cp[o + 4 * ((q + o) >> 4)]; };
+          const uint32_t cbits = __float_as_uint(cp[0]);
           uint32_t lt = 0;
 #pragma unroll
           for (int j = 0; j < REF; ++j)
-            lt += lt_bit(__float_as_uint(cf.alpha * row[midx(d - GUARD - 1 - j)]), cbits) +
-                  lt_bit(__float_as_uint(cf.alpha * row[midx(d + GUARD + 1 + j)]), cbits);
+            lt += lt_bit(__float_as_uint(cf.alpha * ref(-GUARD - 1 - j)), cbits) +
+                  lt_bit(__float_as_uint(cf.alpha * ref(GUARD + 1 + j)), cbits);
           det = (int)lt > cf.rank;
         }
         // in-place ordered compaction: every lane has read its entry of this round, and the
@@ -649,8 +656,8 @@ k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int til
 // after the canceller (MTI on); the last pass stays in registers and feeds |X|^2 (summed over
 // rx: NCI) directly.
 // --------------------------------------------------------------------------------------
-#ifndef FMCW_K2_PREFETCH  // K2 (MTI off) loads the next (tile, rx) unit while it works on this one
-#define FMCW_K2_PREFETCH 1
+#ifndef FMCW_K2_PREFETCH  // K2 (MTI off): points of the next (tile, rx) unit loaded ahead (0, 8 or 16)
+#define FMCW_K2_PREFETCH 16
 #endif
 #ifndef FMCW_K2_ORDER     // K2 tile order (see k_doppler)
 #define FMCW_K2_ORDER 1
@@ -660,7 +667,7 @@ k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int til
 #endif
 template <int NC, int MTI>
 constexpr int k2_waves() {
-  return FMCW_K2_WAVES > 0 ? FMCW_K2_WAVES : (MTI == 0 && NC <= 256 && !FMCW_K2_PREFETCH) ? 3 : 2;
+  return FMCW_K2_WAVES > 0 ? FMCW_K2_WAVES : (MTI == 0 && NC <= 256 && FMCW_K2_PREFETCH <= 8) ? 3 : 2;
 }
 template <int NC, int MTI>
 __global__ void __launch_bounds__(DopplerGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(k2_waves<NC, MTI>())))
@@ -702,7 +709,8 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
   // registers right after this unit's first pass has consumed its own, so a wave keeps 8 KiB
   // of HBM reads in flight through its FFT, magnitude, map store and CFAR phases instead of
   // exposing the full load latency once per unit.
-  constexpr bool PF = MTI == 0 && NC <= 256 && FMCW_K2_PREFETCH;
+  constexpr int NPF = MTI == 0 && NC <= 256 ? FMCW_K2_PREFETCH : 0;  // points loaded ahead
+  constexpr bool PF = NPF > 0;
   // Tile order.  FMCW_K2_ORDER 0: frame-minor over all waves (tile -> f = tile % nf).
   // Measured on config 2: order 1 cuts K2 0.905 -> 0.874 us/frame (map-store cost 0.13 -> 0.085).
   // FMCW_K2_ORDER 1: the WPB waves of a workgroup take WPB consecutive wave tiles (row
@@ -727,14 +735,14 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
     return inter + ((size_t)fu * nrx + rx) * (size_t)ns * NC +
            off_of((uint32_t)(ru >> lgRB) << lgncb, (uint32_t)(ru & ((1 << lgRB) - 1)), 0);
   };
-  float2 nxt[PF ? 16 : 1];
+  float2 nxt[PF ? NPF : 1];
   auto prefetch = [&](int tl, int rx) {
     if constexpr (PF) {
       if (tl < n_tiles) {
         const float2* p = unit_src(tl, rx);
         const int tq = opaque(t0);
 #pragma unroll
-        for (int m = 0; m < 16; ++m) {
+        for (int m = 0; m < NPF; ++m) {
           const uint32_t c = (uint32_t)(tq + P * m);
           nxt[m] = ld_f2<FMCW_NT_SPEC_LD>(p + ((((c >> lgT) << lgRB) << lgT) | (c & (uint32_t)(T - 1))));
         }
@@ -767,7 +775,7 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int c = t + P * m;
-        float2 x = PF ? nxt[m] : at((uint32_t)c);
+        float2 x = m < NPF ? nxt[m < NPF ? m : 0] : at((uint32_t)c);
         if constexpr (MTI >= 2) {  // MTI canceller along slow time, zero history (doppler_notch.vhd:72-102)
           const float2 x1 = c >= 1 ? at((uint32_t)(c - 1)) : make_float2(0.f, 0.f);
           if constexpr (MTI == 2) {
