@@ -109,7 +109,9 @@ __device__ __forceinline__ int opaque(int x) {
 // Cache policy of the streamed HBM traffic (build-time switches, measured by tools/ablate.py
 // against variant builds): NT = non-temporal (`nt` on the global load/store).
 #ifndef FMCW_NT_CUBE      // K1 loads of the input cube (read once)
-#define FMCW_NT_CUBE 0
+// measured on config 2 (tools/ablate.py, 20 steps): K1 0.785 -> 0.667 us/frame (6.29 TB/s),
+// K2 +0.02 us/frame; non-temporal stores of the spectrum instead cost K1 +0.03
+#define FMCW_NT_CUBE 1
 #endif
 #ifndef FMCW_NT_SPEC_ST   // K1 stores of the corner-turned spectrum (re-read by K2)
 #define FMCW_NT_SPEC_ST 0
