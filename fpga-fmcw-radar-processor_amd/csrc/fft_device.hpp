@@ -49,16 +49,11 @@ __device__ __forceinline__ float2 csub(float2 a, float2 b) {
 #ifndef FMCW_PK_CMUL_ASM
 #define FMCW_PK_CMUL_ASM 1
 #endif
-#if defined(FMCW_PK_NOP1) && FMCW_PK_NOP1
-#define FMCW_PK_NOP "s_nop 1\n"
-#else
-#define FMCW_PK_NOP ""
-#endif
 // a * b = (a.x b.x - a.y b.y, a.x b.y + a.y b.x): t = a.x * (b.x, b.y); r = t + (-a.y b.y, a.y b.x)
 #if FMCW_PK_CMUL_ASM
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   fmcw_cf t, r;
-  asm(FMCW_PK_NOP "v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(pk(a)), "v"(pk(b)));
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(pk(a)), "v"(pk(b)));
   asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
       : "=v"(r) : "v"(pk(a)), "v"(pk(b)), "v"(t));
   return unpk(r);
