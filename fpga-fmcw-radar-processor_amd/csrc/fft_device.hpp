@@ -340,6 +340,26 @@ template <int N, int L0> struct FinalRadix {
   static constexpr int G = 16 / R;
 };
 
+// The last pass alone (N / L <= 16) with its twiddle bases supplied by the caller: when
+// P % L == 0 every group of a thread has k = t mod L, so a persistent kernel evaluates the
+// v_sin / v_cos bases once per thread instead of once per transform.
+template <int N, int L, int P>
+__device__ __forceinline__ void stockham_last_tw(const float2* buf, int t, float2 (*out)[N / L],
+                                                 const GroupTwiddles<N / L, N>& tw) {
+  constexpr int R = N / L;
+  constexpr int G = N / R / P;
+  static_assert(R <= 16 && P % L == 0, "one pass, group-invariant twiddles");
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const float2* src = buf + pad16(t + P * g);
+#pragma unroll
+    for (int m = 0; m < R; ++m) out[g][m] = src[padoff(m * (N / R))];
+#pragma unroll
+    for (int m = 1; m < R; ++m) out[g][m] = cmul(out[g][m], tw.pow(m));
+    Dft<R>::run(out[g]);
+  }
+}
+
 // All passes from sub-transform size L except the last, which stays in registers: on
 // return out[g][m] holds X[d] for d = (t + P g) + m * (N / R), R = FinalRadix<N, L>::R.
 template <int N, int L, int P, bool WG_SYNC>

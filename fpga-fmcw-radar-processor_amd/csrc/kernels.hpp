@@ -736,6 +736,10 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
            off_of((uint32_t)(ru >> lgRB) << lgncb, (uint32_t)(ru & ((1 << lgRB) - 1)), 0);
   };
   float2 nxt[PF ? NPF : 1];
+  // last-pass twiddle bases, once per lane (NC = 256: pass 1 + one radix-16 pass, k = t)
+  constexpr bool TWH = NC / 16 <= 16 && P % 16 == 0;
+  GroupTwiddles<NC / 16, NC> twh;
+  if constexpr (TWH) twh.init(t0 & 15);
   auto prefetch = [&](int tl, int rx) {
     if constexpr (PF) {
       if (tl < n_tiles) {
@@ -798,7 +802,8 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
       if (rx + 1 < nrx) prefetch(tile, rx + 1);
       else prefetch(tile + tile_step, 0);
       float2 X[LG][LR];
-      stockham_to_regs<NC, 16, P, false>(buf, t, X);
+      if constexpr (TWH) stockham_last_tw<NC, 16, P>(buf, t, X, twh);
+      else stockham_to_regs<NC, 16, P, false>(buf, t, X);
       if (mag_mode == FMCW_MAG_AMBM) {  // uniform: one branch for the whole block
 #pragma unroll
         for (int g = 0; g < LG; ++g)
