@@ -71,10 +71,17 @@ def main():
     if args.frames:
         wl["frames"] = args.frames
     F, ns, nc, nrx = wl["frames"], wl["ns"], wl["nc"], wl["nrx"]
+    # one rank per GPU; the modulo only matters for a rehearsal of N ranks on fewer GPUs
+    # (with FMCW_BENCH_BACKEND=gloo, since RCCL needs distinct devices)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("FMCW_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     core = RadarCore(N_RANGE=ns, N_DOPPLER=nc, N_RX=nrx, in_dtype=wl["dtype"], cfar=wl["cfar"],
                      max_frames=F, chunk_frames=args.chunk, device=local)
@@ -90,17 +97,40 @@ def main():
     del ut
     rd_map = torch.empty((F, ns, nc), dtype=torch.float32, device=dev)
     det_cap = F * 4096
-    dets = torch.empty((det_cap, 4), dtype=torch.int32, device=dev)
-    n_dets = torch.zeros(4, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    # two detection buffers: with the gather on, step i+1 is enqueued before step i's list is
+    # gathered, so the host-side waits of the gather (counts -> sizes) never idle the GPU
+    bufs = [(torch.empty((det_cap, 4), dtype=torch.int32, device=dev), torch.zeros(4, dtype=torch.int32, device=dev))
+            for _ in range(2)]
+    dets, n_dets = bufs[0]
+    cstream = torch.cuda.current_stream(dev)
+    stream = cstream.cuda_stream
     gather = world > 1 and not args.no_gather
-    last = {}
+    gstream = torch.cuda.Stream(dev) if gather else None
+    last = {"i": 0, "pending": None}
+
+    def do_gather(d, nd, ev):
+        # on its own stream after step's kernels (event): the gather's device->host count reads
+        # wait for that step only; its reads of (d, nd) are complete when this returns
+        with torch.cuda.stream(gstream):
+            gstream.wait_event(ev)
+            allr, counts = gather_detections(d, nd[0], first_global)
+            last["total"] = int(allr.shape[0])
 
     def step():
-        core.enqueue(cube.data_ptr(), F, rd_map.data_ptr(), dets.data_ptr(), det_cap, n_dets.data_ptr(), stream)
+        d, nd = bufs[last["i"] % 2]
+        last["i"] += 1
+        core.enqueue(cube.data_ptr(), F, rd_map.data_ptr(), d.data_ptr(), det_cap, nd.data_ptr(), stream)
         if gather:
-            allr, counts = gather_detections(dets, n_dets[0], first_global)
-            last["total"] = int(allr.shape[0])
+            ev = torch.cuda.Event()
+            ev.record(cstream)
+            prev, last["pending"] = last["pending"], (d, nd, ev)
+            if prev is not None:
+                do_gather(*prev)
+
+    def flush():
+        if last["pending"] is not None:
+            prev, last["pending"] = last["pending"], None
+            do_gather(*prev)
 
     def timed(k):
         torch.cuda.synchronize(dev)
@@ -109,6 +139,7 @@ def main():
         t0 = time.perf_counter()
         for _ in range(k):
             step()
+        flush()
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -119,6 +150,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    flush()
     elapsed = timed(args.steps)
     n_det_step = int(n_dets[0].item())
 
@@ -188,7 +220,9 @@ def main():
         "data": "synthetic (tb_radar_core-style point targets + uniform noise, int16-quantised)",
         "config": {"workload": wl["desc"], "frames_per_gpu_step": F, "n_chirps": nc,
                    "n_samples": ns, "n_rx": nrx, "cfar": wl["cfar"], "rd_map": "linear fp32, written",
-                   "detection_gather": "rccl all_gather" if gather else "none (single GPU)",
+                   "detection_gather": (("rccl" if dist.get_backend() == "nccl" else dist.get_backend())
+                                        + " all_gather, one step behind the compute") if gather
+                                       else "none (single GPU)",
                    "parallelism": f"frame-sharded x{world}"},
         "e2e_GBps_algorithmic": round(e2e_bytes * args.steps * world / elapsed / 1e9, 1),
         "detections_per_step": n_det_step,
