@@ -745,10 +745,17 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
       if (tl < n_tiles) {
         const float2* p = unit_src(tl, rx);
         const int tq = opaque(t0);
+        if ((P & (T - 1)) == 0) {  // uniform: chirps t + P m sit a fixed S elements apart
+          const float2* pb = p + ((((uint32_t)tq >> lgT) << lgRB) << lgT) + ((uint32_t)tq & (uint32_t)(T - 1));
+          const uint32_t S = (uint32_t)(P >> lgT) << (lgRB + lgT);
 #pragma unroll
-        for (int m = 0; m < NPF; ++m) {
-          const uint32_t c = (uint32_t)(tq + P * m);
-          nxt[m] = ld_f2<FMCW_NT_SPEC_LD>(p + ((((c >> lgT) << lgRB) << lgT) | (c & (uint32_t)(T - 1))));
+          for (int m = 0; m < NPF; ++m) nxt[m] = ld_f2<FMCW_NT_SPEC_LD>(pb + (size_t)m * S);
+        } else {
+#pragma unroll
+          for (int m = 0; m < NPF; ++m) {
+            const uint32_t c = (uint32_t)(tq + P * m);
+            nxt[m] = ld_f2<FMCW_NT_SPEC_LD>(p + ((((c >> lgT) << lgRB) << lgT) | (c & (uint32_t)(T - 1))));
+          }
         }
       }
     }
