@@ -50,10 +50,94 @@ __device__ __forceinline__ float key2f(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
+#ifndef FMCW_CFAR2D_SCREEN  // phase A as pair screen + exact count of the survivors (1) or exact (0)
+#define FMCW_CFAR2D_SCREEN 1
+#endif
+constexpr int kCfar2dList = 128;  // u32 per wave after the rows: 64 survivor cells + 64 verdicts
+
 template <int NC>
 constexpr size_t cfar2d_smem_bytes(int hr) {
   using G = Cfar2DGeom<NC>;
-  return (size_t)(G::TR + 2 * hr) * G::RS * 4;
+  return (size_t)(G::TR + 2 * hr) * G::RS * 4 + (FMCW_CFAR2D_SCREEN ? G::WPB * kCfar2dList * 4 : 0);
+}
+
+// Phase A screen (compile-time HD / GD): disjoint PAIRS of Doppler-adjacent references.  A pair
+// with fl(s_min * min) >= cut holds 2 references with fl(s_min * ref) >= cut (fl(s x) is
+// monotone), so 2 * #{such pairs} is a lower bound on the exact count and a cell whose bound
+// reaches n_ref - k cannot detect.  A reference row of 2 HD + 1 cells gives HD pairs (its last
+// cell is left out), a guard row two segments of HD - GD cells, (HD - GD) / 2 pairs each.
+// On noise + targets about 5 % of the cells pass (0.6 % pass the exact count) at half the
+// compares; the survivors are then counted exactly, one per lane.
+template <int NC, int HD, int GD>
+__device__ __forceinline__ uint32_t cfar2d_screen(const float* tile, int rl, int d0, const Cfar2DArgs& a,
+                                                  int need) {
+  constexpr int RS = Cfar2DGeom<NC>::RS;
+  static_assert(HD <= MH, "the window stays inside the row halos");
+  constexpr int W = 16 + 2 * HD;
+  constexpr int O0 = floor4(-HD);
+  constexpr int NV = (W + (-HD - O0) + 3) / 4;
+  constexpr int SEG = HD - GD, NPS = SEG / 2;   // guard-row segment length, pairs per segment
+  const float* lb = tile + (rl + a.hr) * RS + midx(d0);
+  uint32_t cb[16], nlt[16];  // cut bits; #{pairs with fl(s_min * min) < cut}
+  {
+    float c[16];
+    load_cells<4>(lb, 0, c);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      cb[i] = __float_as_uint(c[i]);
+      nlt[i] = 0;
+    }
+  }
+  for (int dr = -a.hr; dr <= a.hr; ++dr) {
+    float v[4 * NV];
+    load_cells<NV>(lb + dr * RS, O0, v);
+    uint32_t pm[W - 1];  // pm[k] = fl(s_min * min(cell k, cell k + 1)), cell 0 = d0 - HD
+#pragma unroll
+    for (int k = 0; k < W - 1; ++k)
+      pm[k] = __float_as_uint(a.s_min * fminf(v[-HD - O0 + k], v[-HD - O0 + k + 1]));
+    if (dr >= -a.gr && dr <= a.gr) {  // guard row (uniform branch)
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+#pragma unroll
+        for (int j = 0; j < NPS; ++j)
+          nlt[i] += lt_bit(pm[i + 2 * j], cb[i]) + lt_bit(pm[i + HD + GD + 1 + 2 * j], cb[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+#pragma unroll
+        for (int j = 0; j < HD; ++j) nlt[i] += lt_bit(pm[i + 2 * j], cb[i]);
+    }
+  }
+  const int n_guard = 2 * a.gr + 1;
+  const int np = (2 * a.hr + 1 - n_guard) * HD + n_guard * 2 * NPS;  // pairs per cell
+  uint32_t bits = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) bits |= (2 * (np - (int)nlt[i]) < need ? 1u : 0u) << i;
+  return bits;
+}
+
+// Exact phase-A test of one cell (CUT row rl of the group tile, Doppler d): candidate <=>
+// #{fl(s_min * ref) >= cut} < need.  Addresses: midx(d + dd) with a runtime d.
+template <int NC, int HD, int GD>
+__device__ __forceinline__ bool cfar2d_exact_a(const float* tile, int rl, int d, const Cfar2DArgs& a, int need) {
+  constexpr int RS = Cfar2DGeom<NC>::RS;
+  const float* crow = tile + (rl + a.hr) * RS;
+  const int x = d + MH;
+  auto at = [&](const float* row, int dd) { return row[(x + dd) + (((x + dd) >> 4) << 2)]; };
+  const uint32_t cbits = __float_as_uint(at(crow, 0));
+  uint32_t lt = 0;
+  for (int dr = -a.hr; dr <= a.hr; ++dr) {
+    const float* row = crow + dr * RS;
+    if (dr >= -a.gr && dr <= a.gr) {
+#pragma unroll
+      for (int dd = -HD; dd <= HD; ++dd)
+        if (dd < -GD || dd > GD) lt += lt_bit(__float_as_uint(a.s_min * at(row, dd)), cbits);
+    } else {
+#pragma unroll
+      for (int dd = -HD; dd <= HD; ++dd) lt += lt_bit(__float_as_uint(a.s_min * at(row, dd)), cbits);
+    }
+  }
+  return (int)lt > a.n_ref - need;
 }
 
 // Phase A for a compile-time Doppler extent HD / guard GD; returns this lane's candidate bits.
@@ -218,10 +302,41 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_wg_tiles, int frame0, int 
     const int r = r0 + rlw;
     uint32_t cand = 0;
     if (r >= a.hr && r < ns - a.hr) {
-      if constexpr (HD > 0)
-        cand = cfar2d_phase_a<NC, HD, GD>(tile, rlw, d0, a, need);
-      else
+      if constexpr (HD > 0) {
+        if constexpr (FMCW_CFAR2D_SCREEN) cand = cfar2d_screen<NC, HD, GD>(tile, rlw, d0, a, need);
+        else cand = cfar2d_phase_a<NC, HD, GD>(tile, rlw, d0, a, need);
+      } else {
         cand = cfar2d_phase_a_generic<NC>(tile, rlw, d0, a, need);
+      }
+    }
+    if constexpr (HD > 0 && FMCW_CFAR2D_SCREEN) {
+      // survivors of the screen -> exact test, 64 per round, one per lane, in cell order
+      uint32_t* const lst = reinterpret_cast<uint32_t*>(tile + (Gm::TR + 2 * a.hr) * RS) + wv * kCfar2dList;
+      uint32_t* const ver = lst + 64;
+      const uint32_t scr = cand;
+      cand = 0;
+      int n_s;
+      const int sx = wave_excl_scan(__popc(scr), n_s);
+      for (int base_s = 0; base_s < n_s; base_s += 64) {  // uniform
+        {
+          int o = sx;
+          for (uint32_t m = scr; m; m &= m - 1, ++o)
+            if (o >= base_s && o < base_s + 64) lst[o - base_s] = ((uint32_t)lane << 4) | (uint32_t)__builtin_ctz(m);
+        }
+        pass_sync<false>();
+        if (base_s + lane < n_s) {
+          const uint32_t e = lst[lane];
+          const int src = (int)(e >> 4), i = (int)(e & 15u);
+          ver[lane] = cfar2d_exact_a<NC, HD, GD>(tile, wv * WR + src / TPR, (src % TPR) * 16 + i, a, need) ? 1u : 0u;
+        }
+        pass_sync<false>();
+        {
+          int o = sx;
+          for (uint32_t m = scr; m; m &= m - 1, ++o)
+            if (o >= base_s && o < base_s + 64 && ver[o - base_s]) cand |= 1u << __builtin_ctz(m);
+        }
+        pass_sync<false>();  // the next round rewrites lst / ver
+      }
     }
 
     // ---- Phase B helpers: the wave's view of candidate cell (row l0 / TPR of the wave, d)

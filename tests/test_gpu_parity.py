@@ -251,6 +251,24 @@ def test_cfar2d_brackets_and_override(gpu, override):
     np.testing.assert_array_equal(got, oracle_dets(m, O.Cfar2D(scale_override=override)))
 
 
+@pytest.mark.parametrize("nc", [64, 256])
+def test_cfar2d_screen_many_survivors(gpu, nc):
+    """Phase A's pair screen (cfar2d.hpp) is defeated on purpose: every other Doppler cell is
+    near zero, so every pair minimum is below any cut and about half of a wave's cells survive
+    the screen (several 64-cell rounds of the exact count per wave).  Bit-exact vs oracle."""
+    rng = np.random.default_rng(11 + nc)
+    m = rng.rayleigh(5.0, (2, 128, nc)).astype(np.float32)
+    m[:, :, 1::2] = rng.uniform(0.0, 0.01, (2, 128, nc // 2)).astype(np.float32)
+    m[0, 40, 10] = 300.0
+    m[1, 60, nc - 3] = 250.0
+    with RadarCore(N_RANGE=128, N_DOPPLER=nc, cfar="os2d", max_frames=2) as core:
+        got = run_cfar_stage(core, m)
+    want = oracle_dets(m, O.Cfar2D())
+    np.testing.assert_array_equal(got, want)
+    pos = set(zip(got["range"].tolist(), got["doppler"].tolist()))
+    assert (40, 10) in pos
+
+
 def test_cfar1d_custom_params(gpu):
     rng = np.random.default_rng(9)
     m = rng.rayleigh(1.0, (3, 64, 128)).astype(np.float32)
