@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--gather", default="rccl", choices=["rccl", "torch"],
+                    help="N > 1: libfmcw's RCCL gather-to-root (no host sync) or torch all_gather")
+    ap.add_argument("--no-h2d", action="store_true", help="skip the H2D-inclusive measurement")
     return ap.parse_args()
 
 
@@ -62,7 +65,7 @@ def main():
     import torch
     import torch.distributed as dist
     from fmcw import RadarCore, synth
-    from fmcw.dist import gather_detections
+    from fmcw.dist import RcclGather, gather_detections
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -97,15 +100,37 @@ def main():
     del ut
     rd_map = torch.empty((F, ns, nc), dtype=torch.float32, device=dev)
     det_cap = F * 4096
-    # two detection buffers: with the gather on, step i+1 is enqueued before step i's list is
-    # gathered, so the host-side waits of the gather (counts -> sizes) never idle the GPU
+    # two detection buffers: step i+1 may be enqueued while step i's list is still gathered
     bufs = [(torch.empty((det_cap, 4), dtype=torch.int32, device=dev), torch.zeros(4, dtype=torch.int32, device=dev))
             for _ in range(2)]
     dets, n_dets = bufs[0]
     cstream = torch.cuda.current_stream(dev)
     stream = cstream.cuda_stream
     gather = world > 1 and not args.no_gather
+    gather_kind = None
+    rg = None
+    wire_cap = F * 128                 # records per rank on the wire: 128 per frame (~64 found)
+    use_rccl = args.gather == "rccl" and os.environ.get("FMCW_BENCH_BACKEND", "nccl") == "nccl"
+    if gather and use_rccl:
+        # libfmcw's fmcw_gather_dets: fixed-size ncclSend/ncclRecv to rank 0, device-side
+        # compaction; stream-ordered after the step, no host synchronisation per step
+        try:
+            obj = [RcclGather.make_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            rg = RcclGather(obj[0], world, rank, local)
+            gather_kind = "libfmcw fmcw_gather_dets (RCCL send/recv to rank 0, fixed wire_cap, no host sync)"
+        except Exception as e:  # noqa: BLE001 -- reported, then the torch path is used
+            print(f"rank {rank}: RCCL gather unavailable ({e}); using torch all_gather", file=sys.stderr)
+            rg = None
+    if gather and rg is None:
+        gather_kind = (("rccl" if dist.get_backend() == "nccl" else dist.get_backend())
+                       + " all_gather via torch.distributed, one step behind the compute")
+    root_out = torch.empty((world * wire_cap, 4), dtype=torch.int32, device=dev) if rg is not None else None
+    root_n = torch.zeros(4, dtype=torch.int32, device=dev) if rg is not None else None
     gstream = torch.cuda.Stream(dev) if gather else None
+    # RCCL path: the gather of step i runs on gstream behind step i (event), and step i + 2 (same
+    # detection buffer) waits for it on the device: no host synchronisation anywhere
+    g_done = [None, None]
     last = {"i": 0, "pending": None}
 
     def do_gather(d, nd, ev):
@@ -113,14 +138,26 @@ def main():
         # wait for that step only; its reads of (d, nd) are complete when this returns
         with torch.cuda.stream(gstream):
             gstream.wait_event(ev)
-            allr, counts = gather_detections(d, nd[0], first_global)
+            allr, counts = gather_detections(d, nd[:2], first_global)
             last["total"] = int(allr.shape[0])
 
     def step():
-        d, nd = bufs[last["i"] % 2]
+        b = last["i"] % 2
+        d, nd = bufs[b]
         last["i"] += 1
+        if rg is not None and g_done[b] is not None:
+            cstream.wait_event(g_done[b])
         core.enqueue(cube.data_ptr(), F, rd_map.data_ptr(), d.data_ptr(), det_cap, nd.data_ptr(), stream)
-        if gather:
+        if rg is not None:
+            ev = torch.cuda.Event()
+            ev.record(cstream)
+            gstream.wait_event(ev)
+            rg.gather(d.data_ptr(), nd.data_ptr(), wire_cap, first_global,
+                      root_out.data_ptr() if rank == 0 else None, root_n.data_ptr() if rank == 0 else None,
+                      0, gstream.cuda_stream)
+            g_done[b] = torch.cuda.Event()
+            g_done[b].record(gstream)
+        elif gather:
             ev = torch.cuda.Event()
             ev.record(cstream)
             prev, last["pending"] = last["pending"], (d, nd, ev)
@@ -194,16 +231,82 @@ def main():
                 "avg_launch_ms": round(ms_r / n_r, 5) if n_r else None}
     e2e_bytes = F * (px * b_in + ns * nc * 4) + 16 * n_det_step
 
+    # H2D-inclusive rate: the cube streamed from pinned host memory inside each step (copy of
+    # batch i+1 on a copy stream overlapping the compute of batch i), PCIe-bound by design
+    h2d = None
+    if not args.no_h2d and world == 1:
+        Fh = min(F, 256)
+        host = torch.empty((Fh,) + tuple(cube.shape[1:]), dtype=cube.dtype, pin_memory=True)
+        host.copy_(cube[:Fh].cpu())
+        dbuf = [torch.empty_like(cube[:Fh]) for _ in range(2)]
+        cps = torch.cuda.Stream(dev)
+        used = [None, None]
+        d_h, nd_h = bufs[0]
+        n_h = 8
+
+        def h2d_run():
+            for i in range(n_h):
+                b = i % 2
+                with torch.cuda.stream(cps):
+                    if used[b] is not None:
+                        cps.wait_event(used[b])
+                    dbuf[b].copy_(host, non_blocking=True)
+                    ready = torch.cuda.Event()
+                    ready.record(cps)
+                cstream.wait_event(ready)
+                core.enqueue(dbuf[b].data_ptr(), Fh, rd_map.data_ptr(), d_h.data_ptr(), det_cap, nd_h.data_ptr(),
+                             stream)
+                used[b] = torch.cuda.Event()
+                used[b].record(cstream)
+
+        h2d_run()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        h2d_run()
+        torch.cuda.synchronize(dev)
+        th = time.perf_counter() - t0
+        h2d = {"frames_per_s_per_gpu": round(n_h * Fh / th, 1),
+               "GBps_h2d": round(n_h * host.numel() * host.element_size() / th / 1e9, 1),
+               "sample": f"{n_h} batches of {Fh} frames from pinned host memory, copy/compute overlapped"}
+        del host, dbuf
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, str(REPO / "oracle"))
         import cpu_baseline as cb
-        uu = synth.frames(8, ns, nc, 1, wl["recipe"], seed=1234, dtype="f32")[:, 0]
-        m = cb.measure(ns, nc, lambda b: uu[:b], target_s=args.cpu_seconds, batch=8)
-        cpu = {"value": round(m["frames_per_s"], 2), "unit": "frames/s", "cores": m["workers"],
+        import fmcw_oracle as O
+        # C backend (oracle/fmcw_cpu.c) on the same workload: single core and all allowed cores
+        nt = cb.threads_allowed()
+        batch = max(8, nt)
+        uu = synth.frames(min(16, batch), ns, nc, nrx, wl["recipe"], seed=1234, dtype="f32")
+        if wl["dtype"] != "f32":
+            uu = (uu[..., 0].astype(np.float32) + 1j * uu[..., 1].astype(np.float32)).astype(np.complex64)
+        ucube = np.concatenate([uu] * ((batch + len(uu) - 1) // len(uu)))[:batch]
+        cf = O.Cfar1D() if wl["cfar"] == "os1d" else O.Cfar2D()
+        mc = cb.measure_c(ucube, cf, runs=20, budget_s=args.cpu_seconds / 2)
+        ac = mc["all_core"]
+        cpu = {"value": round(ac["frames_per_s"], 2), "unit": "frames/s", "cores": ac["threads"],
                "kind": "port",
-               "sample": f"{m['frames']} frames of {ns}x{nc} (1 rx) fp32, NumPy/SciPy fp32 port of the oracle "
-                         f"(oracle/cpu_baseline.py), scipy.fft workers={m['workers']}, {m['seconds']:.1f} s"}
+               "single_core_frames_per_s": round(mc["single_core"]["frames_per_s"], 2),
+               "nproc": mc["nproc"], "cpus_allowed": mc["affinity"], "omp_num_threads": mc["omp_num_threads"],
+               "cpu_model": mc["cpu_model"],
+               "sample": (f"C restatement of the oracle (oracle/fmcw_cpu.c, OpenMP, fp32), {batch} frames of "
+                          f"{ns}x{nc}x{nrx} per run, median of {ac['runs']} runs at {ac['threads']} threads and "
+                          f"{mc['single_core']['runs']} runs at 1 thread")}
+        if args.workload == "c2":
+            # config-3 leg (2-D OS-CFAR, 4 rx NCI): one frame per run
+            u3 = synth.frames(1, 4096, 512, 4, "two_targets", seed=1234, dtype="f32")
+            m3 = cb.measure_c(u3, O.Cfar2D(), runs=20, budget_s=args.cpu_seconds / 2)
+            cpu["config3_2d_cfar"] = {
+                "all_core_frames_per_s": round(m3["all_core"]["frames_per_s"], 3),
+                "single_core_frames_per_s": round(m3["single_core"]["frames_per_s"], 3),
+                "threads": m3["all_core"]["threads"],
+                "sample": f"1 frame of 4096x512x4 (NCI, 2-D OS-CFAR) per run, median of "
+                          f"{m3['all_core']['runs']} / {m3['single_core']['runs']} runs"}
+            # the round-1 NumPy/SciPy port, for continuity
+            uu1 = uu[:8, 0] if uu.ndim == 4 else uu[:8]
+            mp = cb.measure(ns, nc, lambda k: uu1[:k], target_s=2.0, batch=8, workers=nt)
+            cpu["numpy_port_frames_per_s"] = round(mp["frames_per_s"], 2)
 
     out = {
         "metric": "radar frames/sec (range-Doppler+CFAR)",
@@ -220,9 +323,7 @@ def main():
         "data": "synthetic (tb_radar_core-style point targets + uniform noise, int16-quantised)",
         "config": {"workload": wl["desc"], "frames_per_gpu_step": F, "n_chirps": nc,
                    "n_samples": ns, "n_rx": nrx, "cfar": wl["cfar"], "rd_map": "linear fp32, written",
-                   "detection_gather": (("rccl" if dist.get_backend() == "nccl" else dist.get_backend())
-                                        + " all_gather, one step behind the compute") if gather
-                                       else "none (single GPU)",
+                   "detection_gather": gather_kind if gather else "none (single GPU)",
                    "parallelism": f"frame-sharded x{world}"},
         "e2e_GBps_algorithmic": round(e2e_bytes * args.steps * world / elapsed / 1e9, 1),
         "detections_per_step": n_det_step,
@@ -230,10 +331,18 @@ def main():
         "kernels": kern,
         "profiled_step_ms": round(elapsed_prof / args.steps * 1e3, 4),
         "cpu_baseline": cpu,
+        "h2d_inclusive_fps": h2d["frames_per_s_per_gpu"] if h2d else None,
+        "h2d_inclusive": h2d,
     }
+    if rg is not None and rank == 0:
+        torch.cuda.synchronize(dev)
+        out["config"]["gathered_records_last_step"] = int(root_n[0].item())
+        out["config"]["gather_lost_last_step"] = int(root_n[1].item())
     if rank == 0:
         print(json.dumps(out), flush=True)
     core.close()
+    if rg is not None:
+        rg.close()
     if world > 1:
         dist.destroy_process_group()
 

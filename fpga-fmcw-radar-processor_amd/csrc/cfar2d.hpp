@@ -31,6 +31,7 @@ struct Cfar2DArgs {
   int n_ref, rank;
   float s_min, sc_min, sc_nom, sc_max;
   int override_;
+  int compat;          // FMCW_COMPAT_CFAR: 17-bit integer cells, integer mean and brackets
 };
 
 template <int NC> struct Cfar2DGeom {
@@ -281,7 +282,7 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_wg_tiles, int frame0, int 
           const int e4 = b + u * NT;
           if (e4 < n4) {
             const int rl = e4 / (NC / 4), d = (e4 - rl * (NC / 4)) * 4;
-            *reinterpret_cast<float4*>(tile + rl * RS + midx(d)) = v[u];
+            *reinterpret_cast<float4*>(tile + rl * RS + midx(d)) = a.compat ? q17x4(v[u]) : nonneg4(v[u]);
           }
         }
       }
@@ -349,10 +350,19 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_wg_tiles, int frame0, int 
       float sum = va + vb;
 #pragma unroll
       for (int x = 32; x >= 1; x >>= 1) sum += __shfl_xor(sum, x, 64);
-      const float mean = sum / (float)a.n_ref;
       if (a.override_) return (float)a.override_;
-      const float half = mean * 0.5f;
-      const float hi = mean + half;
+      float half, hi;
+      if (a.compat) {
+        // integer cells < 2^17, <= 128 of them: every partial sum < 2^24 is exact in fp32.
+        // mean = floor(sum / N_REF) (os_cfar_2d.vhd:189); the bracket add is 17 bits wide (:193)
+        const uint32_t mean = (uint32_t)sum / (uint32_t)a.n_ref;
+        half = (float)(mean >> 1);
+        hi = (float)((mean + (mean >> 1)) & kQ17Mask);
+      } else {
+        const float mean = sum / (float)a.n_ref;
+        half = mean * 0.5f;
+        hi = mean + half;
+      }
       const int n_hi = __popcll(__ballot(oka && va > hi)) + __popcll(__ballot(okb && vb > hi));
       const int n_lo = __popcll(__ballot(oka && va < half)) + __popcll(__ballot(okb && vb < half));
       return (n_hi >= need) ? a.sc_max : (n_lo >= a.rank + 1) ? a.sc_min : a.sc_nom;

@@ -74,6 +74,13 @@ struct fmcw_handle {
   uint32_t* block_sum = nullptr;  // ceil(n_wg_max / 1024) scan blocks
   uint32_t* n_dets_tmp = nullptr;
   size_t n_wg_max = 0;
+  // fmcw_process host-copy staging, grown on demand and kept (no allocator call per frame batch)
+  void* stage_cube = nullptr;
+  size_t stage_cube_bytes = 0;
+  float* stage_map = nullptr;
+  size_t stage_map_bytes = 0;
+  fmcw_det* stage_dets = nullptr;
+  size_t stage_dets_cap = 0;
   // grid sizes
   int grid_range = 0, grid_doppler = 0, grid_cfar = 0;
   size_t cfar2d_smem = 0;
@@ -88,7 +95,7 @@ struct fmcw_handle {
 namespace {
 
 // ---- kernel dispatch tables ------------------------------------------------------------
-using RangeFn = void (*)(const void*, float2*, const float*, const float*, int, int);
+using RangeFn = void (*)(const void*, float2*, const float*, const float*, int, int, float);
 
 template <int N>
 RangeFn range_fn(int dtype, bool q15) {
@@ -116,7 +123,7 @@ RangeInfo range_info(uint32_t n, int dtype, int window = FMCW_WIN_HAMMING) {
 }
 
 using DopplerFn = void (*)(const float2*, const float*, int, int, int, int, int, int, int, float*,
-                           float*, int, Cfar1DArgs, DetSink);
+                           float*, int, int, Cfar1DArgs, DetSink);
 struct DopplerInfo {
   DopplerFn fn;
   int WR, NT;  // range rows per wave tile, threads per workgroup (DopplerGeom::WPB tiles)
@@ -172,11 +179,13 @@ Cfar2DArgs cfar2_args(const fmcw_config& c) {
   a.hr = (int)(c.cfar2d_ref_range + c.cfar2d_guard_range);
   a.hd = (int)(c.cfar2d_ref_doppler + c.cfar2d_guard_doppler);
   a.n_ref = (2 * a.hr + 1) * (2 * a.hd + 1) - (2 * a.gr + 1) * (2 * a.gd + 1);
-  a.rank = std::min((int)((a.n_ref * (int)c.cfar2d_rank_pct) / 100), a.n_ref - 1);
+  // rank_idx = N_REF * RANK_PCT / 100, clamped to N_REF - 1 (os_cfar_2d.vhd:181-182); 64-bit
+  a.rank = (int)std::min<int64_t>((int64_t)a.n_ref * c.cfar2d_rank_pct / 100, (int64_t)a.n_ref - 1);
   a.sc_min = (float)c.cfar2d_scale_min;
   a.sc_nom = (float)c.cfar2d_scale_nom;
   a.sc_max = (float)c.cfar2d_scale_max;
   a.override_ = (int)c.cfar2d_scale_override;
+  a.compat = (c.compat_rtl & FMCW_COMPAT_CFAR) != 0;
   a.s_min = a.override_ ? (float)a.override_ : std::min(a.sc_min, std::min(a.sc_nom, a.sc_max));
   return a;
 }
@@ -188,6 +197,7 @@ Cfar1DArgs cfar1_args(const fmcw_config& c) {
   a.guard = (int)c.cfar1d_guard;
   a.rank = (int)c.cfar1d_rank;
   a.alpha = c.cfar1d_alpha;
+  a.compat = (c.compat_rtl & FMCW_COMPAT_CFAR) != 0;
   return a;
 }
 
@@ -232,7 +242,14 @@ int validate(const fmcw_config& c) {
     if (2 * (c.cfar1d_ref + c.cfar1d_guard) + 1 > c.n_doppler)
       return fail(FMCW_EINVAL, "1-D CFAR window wider than n_doppler");
     if (!(c.cfar1d_alpha > 0.f)) return fail(FMCW_EINVAL, "1-D CFAR alpha must be > 0");
+    if ((c.compat_rtl & FMCW_COMPAT_CFAR) &&
+        !(c.cfar1d_alpha == std::floor(c.cfar1d_alpha) && c.cfar1d_alpha <= 16384.f))
+      return fail(FMCW_EINVAL, "compat CFAR: alpha is the integer SCALING_MULT (1..16384)");
   } else if (c.cfar_kind == FMCW_CFAR_OS2D) {
+    if (c.cfar2d_rank_pct > 100) return fail(FMCW_EINVAL, "2-D CFAR: rank_pct %u > 100", c.cfar2d_rank_pct);
+    if (c.cfar2d_ref_range > 64 || c.cfar2d_ref_doppler > 64 || c.cfar2d_guard_range > 64 ||
+        c.cfar2d_guard_doppler > 64)
+      return fail(FMCW_EINVAL, "2-D CFAR window extents out of range");
     const Cfar2DArgs a = cfar2_args(c);
     if (a.n_ref < 1 || a.n_ref > 128)
       return fail(FMCW_EINVAL, "2-D CFAR: %d reference cells (supported 1..128)", a.n_ref);
@@ -245,13 +262,18 @@ int validate(const fmcw_config& c) {
   } else if (c.cfar_kind != FMCW_CFAR_NONE) {
     return fail(FMCW_EINVAL, "cfar_kind=%d unknown", c.cfar_kind);
   }
+  if (c.compat_rtl & ~(uint32_t)(FMCW_COMPAT_CFAR | FMCW_COMPAT_MTI))
+    return fail(FMCW_EINVAL, "compat_rtl=0x%x: unknown bits", c.compat_rtl);
+  if ((c.compat_rtl & FMCW_COMPAT_MTI) && c.mti_mode == FMCW_MTI_OFF)
+    return fail(FMCW_EINVAL, "compat MTI needs mti_mode 2 or 3");
+  if (c.range_shift > 13) return fail(FMCW_EINVAL, "range_shift=%u: must be in [0, 13]", c.range_shift);
   return FMCW_OK;
 }
 
 // fp32 window table: Hamming with the RTL's half-ROM mirrored address, computed in fp64
 // (window_multiplier.vhd:34-49, :97-102).  WIN_NONE uploads ones.
-std::vector<float> window_table(uint32_t n, int kind) {
-  std::vector<float> w(n, 1.0f);
+std::vector<float> window_table(uint32_t n, int kind, uint32_t shift = 0) {
+  std::vector<float> w(n, std::ldexp(1.0f, -(int)shift));  // 2^-shift: exact
   if (kind == FMCW_WIN_Q15_RTL) {  // ROM integers c = integer(w * 32767) (:43-46), mirrored
     const uint32_t half = n / 2;
     for (uint32_t i = 0; i < n; ++i) {
@@ -265,7 +287,7 @@ std::vector<float> window_table(uint32_t n, int kind) {
     for (uint32_t i = 0; i < n; ++i) {
       uint32_t a = i < half ? i : n - 1 - i;
       if (a > half - 1) a = half - 1;
-      w[i] = (float)(0.54 - 0.46 * std::cos(2.0 * M_PI * (double)a / (double)(n - 1)));
+      w[i] = std::ldexp((float)(0.54 - 0.46 * std::cos(2.0 * M_PI * (double)a / (double)(n - 1))), -(int)shift);
     }
   }
   return w;
@@ -384,6 +406,11 @@ int launch_det_finish(fmcw_handle* h, size_t n_frames, fmcw_det* dets, size_t de
   return rc;
 }
 
+// 2^-range_shift for the Q15 window path (the fp32 window tables carry it otherwise)
+float q15_scale(const fmcw_config& c) {
+  return c.window == FMCW_WIN_Q15_RTL ? std::ldexp(1.0f, -(int)c.range_shift) : 1.0f;
+}
+
 size_t cube_bytes(const fmcw_config& c, size_t n_frames) {
   const size_t per = (size_t)c.n_rx * c.n_range * c.n_doppler;
   const size_t eb = c.in_dtype == FMCW_IN_F32 ? 8 : 4;
@@ -400,7 +427,25 @@ bool is_device_ptr(const void* p) {
   return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
 
+// Grow-only device staging owned by the handle (fmcw_process with host buffers).
+template <typename T>
+int ensure_stage(T** p, size_t* have, size_t need_bytes, const char* what) {
+  if (*have >= need_bytes) return FMCW_OK;
+  if (*p) hipFree(*p);
+  *p = nullptr;
+  *have = 0;
+  if (hipMalloc(reinterpret_cast<void**>(p), need_bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(FMCW_ENOMEM, "hipMalloc(%zu) for the %s staging buffer failed", need_bytes, what);
+  }
+  *have = need_bytes;
+  return FMCW_OK;
+}
+
 }  // namespace
+
+// the thread-local fmcw_last_error() message, for the other translation units of the library
+int fmcw_internal_fail(int code, const char* msg) { return fail(code, "%s", msg); }
 
 // =======================================================================================
 extern "C" {
@@ -513,7 +558,9 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   ALLOC(h->block_sum, ((h->n_wg_max + 1023) / 1024 + 1) * sizeof(uint32_t));
 #undef ALLOC
   {
-    std::vector<float> wr = window_table(c.n_range, c.window), wd = window_table(c.n_doppler, c.window == FMCW_WIN_Q15_RTL ? FMCW_WIN_HAMMING : c.window);
+    // the range table carries the 2^-range_shift scaling (Q15: applied after the integer window)
+    std::vector<float> wr = window_table(c.n_range, c.window, c.window == FMCW_WIN_Q15_RTL ? 0 : c.range_shift),
+                       wd = window_table(c.n_doppler, c.window == FMCW_WIN_Q15_RTL ? FMCW_WIN_HAMMING : c.window);
     if (hipMemcpy(h->win_r, wr.data(), wr.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(h->win_d, wd.data(), wd.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(h->wg_count, 0, h->n_wg_max * sizeof(uint32_t)) != hipSuccess)
@@ -542,7 +589,8 @@ int fmcw_destroy(fmcw_handle* h) {
   if (!h) return FMCW_OK;
   hipSetDevice(h->cfg.device_id);
   void* ptrs[] = {h->win_r, h->win_d, h->inter, h->lin_scratch, h->det_scratch, h->counter,
-                  h->n_dets_tmp, h->wg_base, h->wg_count, h->wg_off, h->block_sum};
+                  h->n_dets_tmp, h->wg_base, h->wg_count, h->wg_off, h->block_sum,
+                  h->stage_cube, h->stage_map, h->stage_dets};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& pe : h->pending) {
@@ -562,6 +610,7 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
     return fail(FMCW_EINVAL, "n_frames=%zu outside [1, max_frames=%u]", n_frames, c.max_frames);
   if (c.cfar_kind != FMCW_CFAR_NONE && !n_dets_dev)
     return fail(FMCW_EINVAL, "n_dets_dev is required when a CFAR is configured");
+  HIP_TRY(hipSetDevice(c.device_id));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window);
   const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode);
@@ -581,7 +630,7 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
       // MTI off: K1 applies the Doppler window too (k_doppler<NC, 0> expects it)
       const float* chirp_w = c.mti_mode == FMCW_MTI_OFF ? h->win_d : nullptr;
       hipLaunchKernelGGL(ri.fn, dim3(std::min(n_groups, h->grid_range)), dim3(ri.NT), 0, s, src, h->inter,
-                         h->win_r, chirp_w, (int)c.n_doppler, n_groups);
+                         h->win_r, chirp_w, (int)c.n_doppler, n_groups, q15_scale(c));
       if ((rc = check_launch("k_range"))) return rc;
     }
     float* lin = nullptr;
@@ -595,7 +644,8 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
       ProfScope ps(h, FMCW_K_DOPPLER, s);
       hipLaunchKernelGGL(di.fn, dim3(grid), dim3(di.NT), 0, s, h->inter,
                          h->win_d, (int)c.n_range, (int)c.n_rx, h->lgT, h->lgRB, n_tiles, (int)f0,
-                         (int)(f0 * (c.n_range / di.WR)), lin, db, c.mag_mode, cf1, sink);
+                         (int)(f0 * (c.n_range / di.WR)), lin, db, c.mag_mode,
+                         (c.compat_rtl & FMCW_COMPAT_MTI) ? 1 : 0, cf1, sink);
       if ((rc = check_launch("k_doppler"))) return rc;
     }
     if (c.cfar_kind == FMCW_CFAR_OS2D) {
@@ -616,51 +666,36 @@ int fmcw_process(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const size_t cb = cube_bytes(c, n_frames);
   const size_t map_bytes = n_frames * (size_t)c.n_range * c.n_doppler * sizeof(float);
-  void* d_cube = const_cast<void*>(cube);
+  const void* d_cube = cube;
   float* d_map = rd_map;
   fmcw_det* d_dets = dets;
-  std::vector<void*> owned;
-  auto release = [&]() {
-    for (void* p : owned) hipFree(p);
-  };
+  int rc;
   if (!is_device_ptr(cube)) {
-    HIP_TRY(hipMalloc(&d_cube, cb));
-    owned.push_back(d_cube);
-    if (hipMemcpyAsync(d_cube, cube, cb, hipMemcpyHostToDevice, s) != hipSuccess) {
-      release();
-      return fail(FMCW_EHIP, "cube upload failed");
-    }
+    if ((rc = ensure_stage(&h->stage_cube, &h->stage_cube_bytes, cb, "cube"))) return rc;
+    HIP_TRY(hipMemcpyAsync(h->stage_cube, cube, cb, hipMemcpyHostToDevice, s));
+    d_cube = h->stage_cube;
   }
   if (rd_map && !is_device_ptr(rd_map)) {
-    if (hipMalloc(reinterpret_cast<void**>(&d_map), map_bytes) != hipSuccess) {
-      release();
-      return fail(FMCW_ENOMEM, "map scratch");
-    }
-    owned.push_back(d_map);
+    if ((rc = ensure_stage(&h->stage_map, &h->stage_map_bytes, map_bytes, "map"))) return rc;
+    d_map = h->stage_map;
   }
   if (dets && det_cap && !is_device_ptr(dets)) {
-    if (hipMalloc(reinterpret_cast<void**>(&d_dets), det_cap * sizeof(fmcw_det)) != hipSuccess) {
-      release();
-      return fail(FMCW_ENOMEM, "det scratch");
-    }
-    owned.push_back(d_dets);
+    size_t have = h->stage_dets_cap * sizeof(fmcw_det);
+    if ((rc = ensure_stage(&h->stage_dets, &have, det_cap * sizeof(fmcw_det), "detection"))) return rc;
+    h->stage_dets_cap = have / sizeof(fmcw_det);
+    d_dets = h->stage_dets;
   }
-  int rc = fmcw_enqueue(h, d_cube, n_frames, d_map, d_dets, det_cap, h->n_dets_tmp, stream);
-  if (rc) {
-    release();
-    return rc;
-  }
+  if ((rc = fmcw_enqueue(h, d_cube, n_frames, d_map, d_dets, det_cap, h->n_dets_tmp, stream))) return rc;
   uint32_t ndd[2] = {0, 0};  // found, dropped
-  uint32_t& nd = ndd[0];
   hipError_t e = hipSuccess;
   if (c.cfar_kind != FMCW_CFAR_NONE)
     e = hipMemcpyAsync(ndd, h->n_dets_tmp, sizeof ndd, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess && rd_map && d_map != rd_map)
     e = hipMemcpyAsync(rd_map, d_map, map_bytes, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
+  const uint32_t nd = ndd[0];
   if (e == hipSuccess && dets && d_dets != dets && nd)
     e = hipMemcpy(dets, d_dets, std::min<size_t>(nd, det_cap) * sizeof(fmcw_det), hipMemcpyDeviceToHost);
-  release();
   if (e != hipSuccess) return fail(FMCW_EHIP, "fmcw_process: %s", hipGetErrorString(e));
   if (n_dets) *n_dets = nd;
   if (c.cfar_kind != FMCW_CFAR_NONE && (nd > det_cap || ndd[1] > 0))
@@ -673,6 +708,7 @@ int fmcw_range_ct(fmcw_handle* h, const void* cube, size_t n_frames, void* spec,
   if (!h || !cube || !spec) return fail(FMCW_EINVAL, "null argument");
   const fmcw_config& c = h->cfg;
   if (n_frames < 1 || n_frames > c.max_frames) return fail(FMCW_EINVAL, "n_frames out of range");
+  HIP_TRY(hipSetDevice(c.device_id));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window);
   const size_t in_frame_bytes = cube_bytes(c, 1);
@@ -684,7 +720,7 @@ int fmcw_range_ct(fmcw_handle* h, const void* cube, size_t n_frames, void* spec,
       ProfScope ps(h, FMCW_K_RANGE, s);
       hipLaunchKernelGGL(ri.fn, dim3(std::min(n_groups, h->grid_range)), dim3(ri.NT), 0, s,
                          static_cast<const char*>(cube) + f0 * in_frame_bytes, h->inter, h->win_r,
-                         (const float*)nullptr, (int)c.n_doppler, n_groups);
+                         (const float*)nullptr, (int)c.n_doppler, n_groups, q15_scale(c));
       int rc = check_launch("k_range");
       if (rc) return rc;
     }
@@ -714,6 +750,7 @@ int fmcw_cfar(fmcw_handle* h, const float* map, size_t n_frames, fmcw_det* dets,
   const fmcw_config& c = h->cfg;
   if (c.cfar_kind == FMCW_CFAR_NONE) return fail(FMCW_EINVAL, "handle has cfar_kind NONE");
   if (n_frames < 1 || n_frames > c.max_frames) return fail(FMCW_EINVAL, "n_frames out of range");
+  HIP_TRY(hipSetDevice(c.device_id));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   HIP_TRY(hipMemsetAsync(h->counter, 0, 2 * sizeof(uint32_t), s));
   int rc = launch_cfar(h, map, (int)n_frames, 0, s);
@@ -729,6 +766,7 @@ int fmcw_set_profiling(fmcw_handle* h, int enable) {
 
 int fmcw_kernel_times(fmcw_handle* h, double* ms, uint64_t* launches) {
   if (!h) return fail(FMCW_EINVAL, "null handle");
+  HIP_TRY(hipSetDevice(h->cfg.device_id));
   for (auto& pe : h->pending) {
     HIP_TRY(hipEventSynchronize(pe.b));
     float t = 0.f;

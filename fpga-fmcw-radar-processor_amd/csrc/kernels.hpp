@@ -79,7 +79,7 @@ template <int N, typename LD, bool Q15 = false>
 __global__ void __launch_bounds__(RangeGeom<N>::NT)
 __attribute__((amdgpu_waves_per_eu(FMCW_K1_WAVES > 0 && N < 8192 ? FMCW_K1_WAVES : 1)))
 k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* __restrict__ win,
-        const float* __restrict__ chirp_w, int nc, int n_groups) {
+        const float* __restrict__ chirp_w, int nc, int n_groups, float q15_scale) {
   using Gm = RangeGeom<N>;
   constexpr int P = Gm::P, T = Gm::T, RB = Gm::RB, REG = Gm::REG;
   __shared__ __attribute__((aligned(16))) float2 lds[T * REG];
@@ -133,7 +133,8 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
             const int y = ((int)x * c + (1 << 14)) >> 14;  // floor: arithmetic shift
             return (float)min(max(y, -32768), 32767);
           };
-          v[m] = make_float2(win16(xi) * cw, win16(xq) * cw);
+          // 2^-range_shift (the IP's scaling schedule) applies after the integer window
+          v[m] = make_float2(win16(xi) * (cw * q15_scale), win16(xq) * (cw * q15_scale));
         } else {
           const float we = (e ? w[m].y : w[m].x) * cw;
           v[m] = e ? make_float2(a[m].z * we, a[m].w * we) : make_float2(a[m].x * we, a[m].y * we);
@@ -276,10 +277,24 @@ __device__ __forceinline__ int block_excl_scan(int v, int* s_wave, int& total) {
 // reference's unsigned magnitude stream (magnitude_calc.vhd).  No VCC / SGPR mask involved.
 __device__ __forceinline__ uint32_t lt_bit(uint32_t xb, uint32_t yb) { return (xb - yb) >> 31; }
 
+// Caller-supplied maps (fmcw_cfar) enter the CFAR as the RTL's unsigned magnitude stream:
+// negative cells and -0.0 become +0 (integer max on the bit pattern: every pattern with the
+// sign bit set is negative as an int32), so the bit-pattern compares above stay exact.
+__device__ __forceinline__ float nonneg(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
+__device__ __forceinline__ float4 nonneg4(float4 v) {
+  return make_float4(nonneg(v.x), nonneg(v.y), nonneg(v.z), nonneg(v.w));
+}
+// RTL-compat cell (FMCW_COMPAT_CFAR): the 17-bit unsigned CFAR input word (DATA_WIDTH 17,
+// os_cfar.vhd:13, os_cfar_2d.vhd:11), q = min(floor(max(x, 0)), 2^17 - 1); exact in fp32.
+constexpr uint32_t kQ17Mask = (1u << 17) - 1u;
+__device__ __forceinline__ float q17(float x) { return fminf(floorf(nonneg(x)), (float)kQ17Mask); }
+__device__ __forceinline__ float4 q17x4(float4 v) { return make_float4(q17(v.x), q17(v.y), q17(v.z), q17(v.w)); }
+
 struct Cfar1DArgs {
   int enabled;
   int ref, guard, rank;
   float alpha;
+  int compat;        // FMCW_COMPAT_CFAR: 17-bit integer cells, T = (ranked * alpha) mod 2^17
 };
 
 // --------------------------------------------------------------------------------------
@@ -599,12 +614,80 @@ __device__ __forceinline__ void cfar1d_wave(const float* mags, uint32_t* list, i
   }
 }
 
+// RTL-compat 1-D threshold of cell d (rtl/old/os_cfar.vhd:117-132): the 2 ref integer cells
+// q17(.) around d (circular), the rank-th smallest by counting (lt <= rank < le picks it, ties
+// included), T = (ranked * SCALING_MULT / SCALING_DIV) resized to 17 bits = mod 2^17.
+template <int NC>
+__device__ __forceinline__ uint32_t rtl1d_threshold(const float* mrow, int d, const Cfar1DArgs& cf) {
+  const int nref = 2 * cf.ref;
+  uint32_t ranked = 0;
+  for (int j = 0; j < nref; ++j) {
+    const int oj = j < cf.ref ? -(cf.guard + 1 + j) : (cf.guard + 1 + j - cf.ref);
+    const float vj = q17(mrow[midx((d + oj) & (NC - 1))]);
+    int lt = 0, le = 0;
+    for (int i2 = 0; i2 < nref; ++i2) {
+      const int o2 = i2 < cf.ref ? -(cf.guard + 1 + i2) : (cf.guard + 1 + i2 - cf.ref);
+      const float v2 = q17(mrow[midx((d + o2) & (NC - 1))]);
+      lt += v2 < vj;
+      le += v2 <= vj;
+    }
+    if (lt <= cf.rank && cf.rank < le) ranked = (uint32_t)vj;
+  }
+  return (ranked * (uint32_t)cf.alpha) & kQ17Mask;
+}
+
+// 1-D OS-CFAR in RTL-compat arithmetic (FMCW_COMPAT_CFAR) over a wave tile's magnitude rows:
+// detect q17(cut) > T with the wrapped 17-bit threshold, which is not monotone in the ranked
+// cell, so every cell gets its exact ranked value (no screen).  Same ordered emission as
+// cfar1d_wave.
+template <int NC>
+__device__ __forceinline__ void cfar1d_wave_rtl(const float* mags, uint32_t* list, int rr, int t, int r0,
+                                                int frame, int tile, const Cfar1DArgs& cf,
+                                                const DetSink& sink) {
+  constexpr int RS = DopplerGeom<NC>::REGM;
+  const float* mrow = mags + rr * RS;
+  const int d0 = t * 16;
+  const int lane = (int)(threadIdx.x & 63);
+  uint32_t bits = 0;
+  for (int i = 0; i < 16; ++i) {
+    const int d = d0 + i;
+    const uint32_t cut = (uint32_t)q17(mrow[midx(d)]);
+    bits |= (cut > rtl1d_threshold<NC>(mrow, d, cf) ? 1u : 0u) << i;
+  }
+  int total;
+  const int excl = wave_excl_scan(__popc(bits), total);
+  {
+    int o = excl;
+    for (uint32_t m = bits; m; m &= m - 1, ++o) list[o] = ((uint32_t)rr << 16) | (uint32_t)(d0 + __builtin_ctz(m));
+  }
+  const uint32_t base = det_reserve_wave(sink, tile, total);
+  if (total == 0) return;  // uniform
+  pass_sync<false>();
+  for (int i = lane; i < total; i += 64) {
+    const uint32_t cell = list[i];
+    const int rl = (int)(cell >> 16), d = (int)(cell & 0xffffu);
+    const float* row = mags + rl * RS;
+    const uint32_t slot = base + (uint32_t)i;
+    if (slot < sink.cap) {
+      fmcw_det dd;
+      dd.frame = (uint32_t)frame;
+      dd.range = (uint16_t)(r0 + rl);
+      dd.doppler = (uint16_t)d;
+      dd.mag = q17(row[midx(d)]);
+      dd.threshold = (float)rtl1d_threshold<NC>(row, d, cf);
+      sink.scratch[slot] = dd;
+    }
+  }
+}
+
 // Dispatch on the compile-time fast path (the reference geometry REF 8 / GUARD 2).
 template <int NC>
 __device__ __forceinline__ void cfar1d_dispatch(const float* mags, uint32_t* list, int rr, int t, int r0,
                                                 int frame, int tile, const Cfar1DArgs& cf,
                                                 const DetSink& sink) {
-  if (cf.ref == 8 && cf.guard == 2)
+  if (cf.compat)
+    cfar1d_wave_rtl<NC>(mags, list, rr, t, r0, frame, tile, cf, sink);
+  else if (cf.ref == 8 && cf.guard == 2)
     cfar1d_wave<NC, 8, 2>(mags, list, rr, t, r0, frame, tile, cf, sink);
   else
     cfar1d_wave<NC, 0, 0>(mags, list, rr, t, r0, frame, tile, cf, sink);
@@ -636,7 +719,7 @@ k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int til
     for (int i = 0; i < WR * NC / 4 / 64; ++i) {
       const int e = 4 * (lane + 64 * i);
       const int rl = e / NC, d = e - rl * NC;
-      *reinterpret_cast<float4*>(mags + rl * REGM + midx(d)) = *reinterpret_cast<const float4*>(src + e);
+      *reinterpret_cast<float4*>(mags + rl * REGM + midx(d)) = nonneg4(*reinterpret_cast<const float4*>(src + e));
     }
     pass_sync<false>();
     fill_halo<NC, P>(mags + (lane / P) * REGM, lane % P);
@@ -656,6 +739,12 @@ k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int til
 // after the canceller (MTI on); the last pass stays in registers and feeds |X|^2 (summed over
 // rx: NCI) directly.
 // --------------------------------------------------------------------------------------
+// FMCW_COMPAT_MTI word format: round half to even (the IP's convergent rounding) and saturate
+// to int16, per component; and the canceller's output saturation (doppler_notch.vhd:75-93).
+__device__ __forceinline__ float sat16(float v) { return fminf(fmaxf(v, -32768.f), 32767.f); }
+__device__ __forceinline__ float2 sat16c(float2 v) { return make_float2(sat16(v.x), sat16(v.y)); }
+__device__ __forceinline__ float2 q16c(float2 v) { return make_float2(sat16(rintf(v.x)), sat16(rintf(v.y))); }
+
 #ifndef FMCW_K2_PREFETCH  // K2 (MTI off): points of the next (tile, rx) unit loaded ahead (0, 8 or 16)
 #define FMCW_K2_PREFETCH 16
 #endif
@@ -673,7 +762,7 @@ template <int NC, int MTI>
 __global__ void __launch_bounds__(DopplerGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(k2_waves<NC, MTI>())))
 k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int ns, int nrx,
           int lgT, int lgRB, int n_tiles, int frame0, int tile0, float* __restrict__ lin_map,
-          float* __restrict__ db_map, int mag_mode, Cfar1DArgs cf, DetSink sink) {
+          float* __restrict__ db_map, int mag_mode, int mti_rtl, Cfar1DArgs cf, DetSink sink) {
   using Gm = DopplerGeom<NC>;
   constexpr int P = Gm::P, WR = Gm::WR, WPB = Gm::WPB, REGD = Gm::REGD, REGM = Gm::REGM;
   constexpr int LR = Gm::LR, LG = Gm::LG;
@@ -788,13 +877,17 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
         const int c = t + P * m;
         float2 x = m < NPF ? nxt[m < NPF ? m : 0] : at((uint32_t)c);
         if constexpr (MTI >= 2) {  // MTI canceller along slow time, zero history (doppler_notch.vhd:72-102)
-          const float2 x1 = c >= 1 ? at((uint32_t)(c - 1)) : make_float2(0.f, 0.f);
-          if constexpr (MTI == 2) {
-            x = csub(x, x1);
-          } else {
-            const float2 x2 = c >= 2 ? at((uint32_t)(c - 2)) : make_float2(0.f, 0.f);
-            x = cadd(csub(x, cscale(x1, 2.f)), x2);
+          float2 x1 = c >= 1 ? at((uint32_t)(c - 1)) : make_float2(0.f, 0.f);
+          float2 x2 = make_float2(0.f, 0.f);
+          if constexpr (MTI == 3) x2 = c >= 2 ? at((uint32_t)(c - 2)) : make_float2(0.f, 0.f);
+          if (mti_rtl) {  // FMCW_COMPAT_MTI: 16-bit words in, saturating integer difference out
+            x = q16c(x);
+            x1 = q16c(x1);
+            x2 = q16c(x2);
           }
+          // integers below 2^18 in compat mode: every step below is exact
+          x = MTI == 2 ? csub(x, x1) : cadd(csub(x, cscale(x1, 2.f)), x2);
+          if (mti_rtl) x = sat16c(x);
         }
         if constexpr (MTI != 0) x = cscale(x, wv_d[m]);
         v[m] = x;

@@ -23,6 +23,8 @@ MAG_ABS, MAG_AMBM = 0, 1
 MAP_LINEAR, MAP_DB = 1, 2
 CFAR_NONE, CFAR_OS1D, CFAR_OS2D = 0, 1, 2
 MTI_OFF, MTI_2PULSE, MTI_3PULSE = 0, 2, 3
+COMPAT_CFAR, COMPAT_MTI = 1, 2
+COMM_ID_BYTES = 128
 K_RANGE, K_DOPPLER, K_CFAR2D, K_COMPACT, K_COUNT = 0, 1, 2, 3, 4
 KERNEL_NAMES = ("k_range", "k_doppler", "k_cfar", "k_compact")
 
@@ -43,6 +45,7 @@ class FmcwConfig(C.Structure):
         ("cfar2d_scale_nom", C.c_uint32), ("cfar2d_scale_max", C.c_uint32),
         ("cfar2d_scale_override", C.c_uint32),
         ("max_frames", C.c_uint32), ("chunk_frames", C.c_uint32), ("device_id", C.c_int32),
+        ("compat_rtl", C.c_uint32), ("range_shift", C.c_uint32),
     ]
 
 
@@ -84,6 +87,10 @@ SIGNATURES = {
     "fmcw_device_free": (_I, [_VP]),
     "fmcw_memcpy": (_I, [_VP, _VP, _SZ, _I]),
     "fmcw_device_count": (_I, [C.POINTER(_I)]),
+    "fmcw_comm_unique_id": (_I, [_VP]),
+    "fmcw_comm_create": (_I, [_VP, _I, _I, _I, C.POINTER(_VP)]),
+    "fmcw_comm_destroy": (_I, [_VP]),
+    "fmcw_gather_dets": (_I, [_VP, _VP, _VP, _SZ, C.c_uint32, _VP, _VP, _I, _VP]),
     "fmcw_tws_config_default": (None, [C.POINTER(FmcwTwsConfig)]),
     "fmcw_tws_create": (_I, [C.POINTER(FmcwTwsConfig), C.POINTER(_VP)]),
     "fmcw_tws_destroy": (_I, [_VP]),

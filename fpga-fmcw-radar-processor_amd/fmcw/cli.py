@@ -13,6 +13,7 @@ INPUT formats (by extension):
 Outputs in --out-dir (names the visualizer searches, model/visualize_radar_targets.py:37-107):
   ADR_detections.txt (or ADR_quick_det.txt with --quick): "r d mag" per detection
   radar_output.txt (with --map-file): "r d 0 0 mag" map of the first frame
+  --doppler-centred shifts Doppler bins by N/2 (fftshift) in both files
   ADR_tracks.txt (with --tracks): the track-while-scan log, one scan per frame
                  ("TRK id R= D= Q=" / "SCAN_END ACTIVE=n", tb_radar_core.vhd:163-180)
 """
@@ -63,6 +64,8 @@ def main(argv=None):
     ap.add_argument("--tracks", action="store_true", help="run the TWS tracker, write ADR_tracks.txt")
     ap.add_argument("--tracker-rtl", action="store_true", help="tracker in RTL-compat mode")
     ap.add_argument("--window", default="hamming", choices=["hamming", "none", "q15_rtl"])
+    ap.add_argument("--doppler-centred", action="store_true",
+                    help="write Doppler bins fftshifted (zero Doppler at N/2, as the visualizer assumes)")
     a = ap.parse_args(argv)
     cube, dt = load_cube(a.input, a.n_range, a.n_doppler)
     nf = cube.shape[0]
@@ -71,9 +74,10 @@ def main(argv=None):
         out = core.process(np.ascontiguousarray(cube))
     a.out_dir.mkdir(parents=True, exist_ok=True)
     det_name = "ADR_quick_det.txt" if a.quick else "ADR_detections.txt"
-    n = formats.write_detections(a.out_dir / det_name, out.dets)
+    n = formats.write_detections(a.out_dir / det_name, out.dets, doppler_centred=a.doppler_centred,
+                                 n_doppler=a.n_doppler)
     if a.map_file:
-        formats.write_rd_map(a.out_dir / a.map_file, out.rd_map[0])
+        formats.write_rd_map(a.out_dir / a.map_file, out.rd_map[0], doppler_centred=a.doppler_centred)
     print(f"{nf} frame(s) {a.n_doppler}x{a.n_range}: {n} detections -> {a.out_dir / det_name}")
     if a.tracks:
         with TwsTracker(rtl_compat=a.tracker_rtl) as trk:

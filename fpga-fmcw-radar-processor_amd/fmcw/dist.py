@@ -2,14 +2,25 @@
 
 Frames are independent units: frame f of a batch of F goes to rank floor(f * G / F)
 (contiguous blocks), each rank runs the whole hot path on its block with no data-path
-collective.  The only exchange is the detection list, gathered to every rank (or rank 0)
-over RCCL (torch.distributed backend "nccl" on ROCm) in two steps:
-  1. all_gather of the per-rank counts (G x 8 B);
-  2. all_gather_into_tensor of the lists padded to the largest count (16 B records).
+collective.  The only exchange is the detection list.  Two implementations:
+
+  RcclGather          the C-ABI gather of libfmcw.so (fmcw_gather_dets): every rank sends a
+                      fixed-size message (count header + wire_cap records) to the root with
+                      ncclSend/ncclRecv over xGMI, the root compacts on the device.  Stream-
+                      ordered, no host synchronisation per step.  What bench.py uses at N > 1.
+  gather_detections   torch.distributed: all_gather of the counts, then of the lists padded to
+                      the largest count.  Works on any backend (gloo on CPU for the tests);
+                      host-synchronising (the counts decide the padded size).
+
 Records carry the global frame index (local frame + the rank's first frame).
 The reference has no distributed layer (a single FPGA); this is the MI355X-side addition.
 """
 from __future__ import annotations
+
+import ctypes as C
+import warnings
+
+from . import _lib as L
 
 
 def shard_frames(n_frames: int, world: int, rank: int):
@@ -19,13 +30,18 @@ def shard_frames(n_frames: int, world: int, rank: int):
     return lo, hi
 
 
-def gather_detections(dets, n_dets, frame_offset: int, group=None):
-    """Gather detection records from every rank.
+def gather_detections(dets, n_dets, frame_offset: int, group=None, dropped: int = 0):
+    """Gather detection records from every rank (torch.distributed, any backend).
 
-    dets:    uint8/int32 torch tensor holding >= n_dets 16-byte fmcw_det records (device or CPU)
-    n_dets:  python int or 1-element tensor with this rank's count
+    dets:    uint8/int32 torch tensor holding fmcw_det 16-byte records (device or CPU)
+    n_dets:  python int or tensor whose first element is this rank's count of detections
+             found (fmcw.h n_dets_dev[0], which may exceed the buffer), and optionally
+             second element the detections the library could not store (n_dets_dev[1])
+    dropped: records lost upstream, if n_dets carries no second element
     Returns (all_records int32 [total, 4], counts list) on every rank, ordered by rank, i.e.
-    by global frame because shards are contiguous.
+    by global frame because shards are contiguous.  A rank whose list is incomplete (count
+    beyond its buffer, or library-side losses) contributes what it holds and a warning is
+    raised, as fmcw_process reports FMCW_EDETCAP.
     """
     import torch
     import torch.distributed as dist
@@ -33,7 +49,16 @@ def gather_detections(dets, n_dets, frame_offset: int, group=None):
     world = dist.get_world_size(group)
     dev = dets.device
     rec = dets.view(torch.int32).reshape(-1, 4)
-    n = int(n_dets.item()) if hasattr(n_dets, "item") else int(n_dets)
+    if hasattr(n_dets, "tolist"):
+        v = n_dets.reshape(-1).tolist()
+        found = int(v[0])
+        lost = int(v[1]) if len(v) > 1 else int(dropped)
+    else:
+        found, lost = int(n_dets), int(dropped)
+    n = min(found, rec.shape[0])
+    if lost or n < found:
+        warnings.warn(f"rank {dist.get_rank(group)}: detection list incomplete ({found} found, "
+                      f"{rec.shape[0]} buffer rows, {lost} lost in the library scratch)")
     mine = rec[:n].clone()
     if frame_offset:
         mine[:, 0] += frame_offset                  # fmcw_det.frame is the first u32
@@ -49,3 +74,44 @@ def gather_detections(dets, n_dets, frame_offset: int, group=None):
     outs = [torch.empty((m, 4), dtype=torch.int32, device=dev) for _ in range(world)]
     dist.all_gather(outs, pad, group=group)        # one ring all-gather (RCCL / gloo)
     return torch.cat([outs[r][:counts[r]] for r in range(world)]), counts
+
+
+class RcclGather:
+    """fmcw_comm_* / fmcw_gather_dets of include/fmcw.h: gather-to-root over RCCL.
+
+    ``unique_id`` (FMCW_COMM_ID_BYTES bytes from ``RcclGather.make_id()`` on one rank) must be
+    distributed out of band, e.g. with torch.distributed.broadcast_object_list."""
+
+    def __init__(self, unique_id: bytes, n_ranks: int, rank: int, device: int):
+        lib = L.load()
+        if len(unique_id) != L.COMM_ID_BYTES:
+            raise ValueError("unique id must be FMCW_COMM_ID_BYTES long")
+        buf = C.create_string_buffer(bytes(unique_id), L.COMM_ID_BYTES)
+        h = C.c_void_p()
+        L.check(lib.fmcw_comm_create(buf, n_ranks, rank, device, C.byref(h)))
+        self._h, self._lib = h, lib
+        self.n_ranks, self.rank = n_ranks, rank
+
+    @staticmethod
+    def make_id() -> bytes:
+        buf = C.create_string_buffer(L.COMM_ID_BYTES)
+        L.check(L.load().fmcw_comm_unique_id(buf))
+        return buf.raw
+
+    def gather(self, dets_ptr: int, n_dets_ptr: int, wire_cap: int, frame_offset: int,
+               out_ptr: int | None, out_n_ptr: int | None, root: int = 0, stream: int = 0):
+        """Device pointers; asynchronous on `stream`.  On the root, out holds n_ranks * wire_cap
+        records, out_n [0] records written, [1] records lost (a rank over wire_cap)."""
+        L.check(self._lib.fmcw_gather_dets(self._h, dets_ptr, n_dets_ptr, wire_cap, frame_offset,
+                                           out_ptr, out_n_ptr, root, stream or None))
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            self._lib.fmcw_comm_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -7,6 +7,12 @@
   rd map      "r d 0 0 mag" -- 5 columns, range-major, as data/radar_output.txt.
               The visualizer's parser rejects 5-token lines; this is the data/ format.
   ADC input   "I Q" integer pairs, one sample per line, as data/golden_input_chirp.txt.
+
+Doppler order.  The library emits natural FFT order (bin 0 = zero Doppler).
+The visualizer centres zero Doppler at N_DOPPLER/2 (bin_to_velocity_mps,
+visualize_radar_targets.py:174-182) and the ADR stimuli pre-offset by +N/2
+(rtl/old/ADR_tb_quick.vhd:149-157); the writers' ``doppler_centred=True`` applies that
+fftshift, d' = (d + N/2) mod N, so that the visualizer converts zero Doppler to 0 m/s.
 """
 from __future__ import annotations
 
@@ -15,12 +21,23 @@ from pathlib import Path
 import numpy as np
 
 
-def write_detections(path, dets, frame: int | None = None) -> int:
+def centre_doppler(d, n_doppler: int):
+    """Natural-order Doppler bins -> centred order (fftshift): (d + N/2) mod N."""
+    return (np.asarray(d, np.int64) + n_doppler // 2) % n_doppler
+
+
+def write_detections(path, dets, frame: int | None = None, doppler_centred: bool = False,
+                     n_doppler: int | None = None) -> int:
     """Write detections as 'r d mag' integer lines (optionally only one frame's)."""
     d = dets if frame is None else dets[dets["frame"] == frame]
     mag = np.rint(np.asarray(d["mag"], np.float64)).astype(np.int64)
+    dop = np.asarray(d["doppler"], np.int64)
+    if doppler_centred:
+        if not n_doppler:
+            raise ValueError("doppler_centred needs n_doppler")
+        dop = centre_doppler(dop, n_doppler)
     with open(path, "w") as f:
-        for r, dd, m in zip(d["range"].tolist(), d["doppler"].tolist(), mag.tolist()):
+        for r, dd, m in zip(d["range"].tolist(), dop.tolist(), mag.tolist()):
             f.write(f"{r} {dd} {m}\n")
     return len(d)
 
@@ -35,9 +52,11 @@ def read_detections(path) -> np.ndarray:
     return np.array(rows, dtype=np.int64).reshape(-1, 3)
 
 
-def write_rd_map(path, rd_map: np.ndarray) -> None:
+def write_rd_map(path, rd_map: np.ndarray, doppler_centred: bool = False) -> None:
     """One frame [range][doppler] -> 'r d 0 0 mag' lines, range-major, integer magnitudes."""
     m = np.rint(np.asarray(rd_map, np.float64)).astype(np.int64)
+    if doppler_centred:
+        m = np.fft.fftshift(m, axes=-1)         # column d' holds natural bin (d' - N/2) mod N
     nr, nd = m.shape
     r = np.repeat(np.arange(nr), nd)
     d = np.tile(np.arange(nd), nr)

@@ -83,15 +83,21 @@ class DeviceBuffer:
         L.check(L.load().fmcw_device_alloc(self.nbytes, C.byref(p), device))
         self.ptr = p.value
 
-    def upload(self, arr: np.ndarray):
+    def upload(self, arr: np.ndarray, offset: int = 0):
         a = np.ascontiguousarray(arr)
-        assert a.nbytes <= self.nbytes
-        L.check(L.load().fmcw_memcpy(self.ptr, a.ctypes.data, a.nbytes, 0))
+        assert offset + a.nbytes <= self.nbytes
+        L.check(L.load().fmcw_memcpy(self.ptr + offset, a.ctypes.data, a.nbytes, 0))
 
-    def download(self, dtype, shape) -> np.ndarray:
+    def download(self, dtype, shape, offset: int = 0) -> np.ndarray:
         out = np.empty(shape, dtype=dtype)
-        L.check(L.load().fmcw_memcpy(out.ctypes.data, self.ptr, out.nbytes, 1))
+        assert offset + out.nbytes <= self.nbytes
+        L.check(L.load().fmcw_memcpy(out.ctypes.data, self.ptr + offset, out.nbytes, 1))
         return out
+
+    def copy_from(self, src: "DeviceBuffer", nbytes: int, src_offset: int = 0, dst_offset: int = 0):
+        """Device-to-device copy (e.g. tiling a few frames into a large batch)."""
+        assert src_offset + nbytes <= src.nbytes and dst_offset + nbytes <= self.nbytes
+        L.check(L.load().fmcw_memcpy(self.ptr + dst_offset, src.ptr + src_offset, nbytes, 2))
 
     def free(self):
         if self.ptr:
@@ -133,11 +139,16 @@ class RadarCore:
                  cfar1d=(8, 2, 12, 4.0), in_dtype: str = "f32", window: str = "hamming",
                  magnitude: str = "abs", map_kind: str = "linear", max_frames: int = 1,
                  chunk_frames: int = 0, device: int = 0, mti_bypass: bool = True,
-                 NOTCH_MODE: int = 2):
+                 NOTCH_MODE: int = 2, compat_rtl=(), range_shift: int = 0):
         """mti_bypass / NOTCH_MODE mirror radar_core's u_mti (radar_core.vhd:329-338, port
         :48).  The RTL port defaults to '0' (MTI on); this mirror defaults to bypass because
         the north-star path and BASELINE configs exclude MTI and tb_radar_core bypasses it
-        (rtl/src/tb_radar_core.vhd:66)."""
+        (rtl/src/tb_radar_core.vhd:66).
+
+        compat_rtl: RTL-compat arithmetic (fmcw.h fmcw_compat): any of "cfar" (17-bit integer
+        CFAR, os_cfar.vhd:132 / os_cfar_2d.vhd:189-199) and "mti" (int16 saturating canceller,
+        doppler_notch.vhd:73-93).  range_shift: range spectrum scaled by 2^-range_shift (the
+        FFT IP's fixed scaling schedule), so that the MTI's 16-bit words are meaningful."""
         lib = L.load()
         cfg = L.default_config()
         cfg.mti_mode = L.MTI_OFF if mti_bypass else {2: L.MTI_2PULSE, 3: L.MTI_3PULSE}[NOTCH_MODE]
@@ -155,6 +166,10 @@ class RadarCore:
         cfg.cfar2d_scale_min, cfg.cfar2d_scale_nom, cfg.cfar2d_scale_max = cfar_scales
         cfg.cfar2d_scale_override = cfar_scale_ovr
         cfg.max_frames, cfg.chunk_frames, cfg.device_id = max_frames, chunk_frames, device
+        flags = {"cfar": L.COMPAT_CFAR, "mti": L.COMPAT_MTI}
+        cfg.compat_rtl = compat_rtl if isinstance(compat_rtl, int) else \
+            sum(flags[k] for k in set(compat_rtl))
+        cfg.range_shift = range_shift
         self.cfg = cfg
         self.in_dtype = in_dtype
         self.device = device

@@ -32,8 +32,11 @@
  *     and asynchronous (nothing synchronises, nothing allocates: graph-capturable).
  *   - fmcw_process accepts host or device pointers (detected with hipPointerGetAttributes),
  *     and returns after the results are in the caller's buffers.
- *   - A handle is not thread-safe: one handle per host thread.  All scratch is allocated
- *     at fmcw_create for up to cfg.max_frames frames per call.
+ *   - A handle is not thread-safe: one handle per host thread, and one stream at a time
+ *     (its scratch -- intermediate spectrum, detection slots, counters -- is shared by its
+ *     calls, so two calls in flight on different streams race).  Every entry point selects
+ *     the handle's device itself.  All kernel scratch is allocated at fmcw_create for up to
+ *     cfg.max_frames frames per call; fmcw_process keeps its host-copy staging in the handle.
  *   - Layouts (row-major, complex = interleaved re,im):
  *       cube   [frame][rx][chirp][sample]       in_dtype (f32 / f16 / int16 complex)
  *       map    [frame][range][doppler]          float32 (range-major, as radar_output.txt)
@@ -50,7 +53,7 @@
 extern "C" {
 #endif
 
-#define FMCW_ABI_VERSION 1
+#define FMCW_ABI_VERSION 2  /* 2: fmcw_config grew compat_rtl, range_shift (27 words, 108 B) */
 
 typedef enum {
   FMCW_OK = 0,
@@ -110,7 +113,27 @@ typedef struct fmcw_config {
   uint32_t max_frames;     /* largest n_frames per call (scratch is sized for it) */
   uint32_t chunk_frames;   /* frames per internal kernel chunk (0 = auto) */
   int32_t device_id;       /* HIP device ordinal */
+  /* RTL-compat arithmetic, a bitmask of fmcw_compat; 0 = the fp32 build spec */
+  uint32_t compat_rtl;
+  /* range FFT output scaled by 2^-range_shift (exact): the Xilinx IP's fixed scaling schedule
+   * SCALE_SCH (tb_xfft_128.vhd:480-494), so that spectra fit the IP's 16-bit output word;
+   * 0..13 */
+  uint32_t range_shift;
 } fmcw_config;
+
+/* fmcw_config.compat_rtl bits.
+ * FMCW_COMPAT_CFAR: the CFAR on the RTL's 17-bit unsigned cells (DATA_WIDTH 17): each map
+ *   cell enters the CFAR as q = min(floor(max(x, 0)), 2^17 - 1) (the map itself is unchanged).
+ *   1-D (rtl/old/os_cfar.vhd:132-137): T = (ranked * alpha) mod 2^17 (resize to DATA_WIDTH),
+ *   detect q_cut > T; alpha must be an integer (SCALING_MULT, SCALING_DIV = 1).
+ *   2-D (rtl/src/os_cfar_2d.vhd:163, :189-213): mean = floor(sum / n_ref) of the integer refs,
+ *   hi = (mean + (mean >> 1)) mod 2^17 (a 17-bit add), lo = mean >> 1, the same brackets,
+ *   T = ranked * scale at full width.  fmcw_det.mag / .threshold carry q_cut and T.
+ * FMCW_COMPAT_MTI: the MTI canceller on 16-bit words (rtl/src/doppler_notch.vhd:67-93): the
+ *   (range_shift-scaled) spectrum is rounded half-to-even and saturated to int16 (the IP's
+ *   output word, convergent rounding xfft_0.xci), then y = sat16(x - x1) or
+ *   sat16(x - 2 x1 + x2) in integers.  Needs mti_mode != OFF. */
+typedef enum { FMCW_COMPAT_CFAR = 1, FMCW_COMPAT_MTI = 2 } fmcw_compat;
 
 /* One detection: 16 bytes, sorted by (frame, range, doppler). */
 typedef struct fmcw_det {
@@ -164,11 +187,35 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
 int fmcw_process(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_map,
                  fmcw_det* dets, size_t det_cap, size_t* n_dets, void* stream);
 
-/* Stage entry points (device pointers, asynchronous). */
+/* Stage entry points (device pointers, asynchronous).
+ * fmcw_cfar reads the map as the RTL's unsigned magnitude stream (magnitude_calc.vhd:45-88):
+ * negative cells and -0.0 are taken as +0; NaN / Inf cells are unsupported. */
 int fmcw_range_ct(fmcw_handle* h, const void* cube, size_t n_frames, void* spec, void* stream);
 int fmcw_magnitude(const float* iq, float* out, size_t n, int mag_mode, void* stream);
 int fmcw_cfar(fmcw_handle* h, const float* map, size_t n_frames, fmcw_det* dets,
               size_t det_cap, uint32_t* n_dets_dev, void* stream);
+
+/* ---- Multi-GPU detection gather (RCCL over xGMI) ------------------------
+ * The reference is one FPGA and has no distributed layer; this is the optional gather of
+ * frame-sharded detection lists to one root rank.  One process per GPU.  Rank 0 makes the
+ * id (fmcw_comm_unique_id), the caller distributes its FMCW_COMM_ID_BYTES bytes out of band,
+ * every rank calls fmcw_comm_create (collective).
+ * fmcw_gather_dets is stream-ordered and never synchronises with the host: every rank sends
+ * a fixed-size message (a 16-B header holding its count, then `wire_cap` record slots) to
+ * `root` with ncclSend/ncclRecv, and the root compacts the lists on the device in rank order
+ * (= global frame order for contiguous shards).  Each rank's .frame values get `frame_offset`
+ * added (its first global frame).  On the root: out_dev holds n_ranks * wire_cap records,
+ * out_n_dev[0] = records written, out_n_dev[1] = records not sent because a rank had more
+ * than wire_cap (or its n_dets_dev[1] reported scratch losses).  Other ranks may pass NULL
+ * out pointers. */
+#define FMCW_COMM_ID_BYTES 128
+typedef struct fmcw_comm fmcw_comm;
+int fmcw_comm_unique_id(void* id_out);
+int fmcw_comm_create(const void* id, int n_ranks, int rank, int device_id, fmcw_comm** out);
+int fmcw_comm_destroy(fmcw_comm* c);
+int fmcw_gather_dets(fmcw_comm* c, const fmcw_det* dets_dev, const uint32_t* n_dets_dev,
+                     size_t wire_cap, uint32_t frame_offset, fmcw_det* out_dev,
+                     uint32_t* out_n_dev, int root, void* stream);
 
 /* Profiling: when enabled, fmcw_enqueue brackets each kernel launch with hipEvents on
  * its stream; fmcw_kernel_times synchronises and returns, per fmcw_kernel_id, the summed

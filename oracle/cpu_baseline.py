@@ -1,15 +1,22 @@
-"""CPU baseline: the oracle's algorithm as a throughput-oriented fp32 NumPy/SciPy port.
+"""CPU baseline of bench.py: the oracle's algorithm timed on the host cores.
 
-TEST/BENCH INFRASTRUCTURE ONLY (bench.py's cpu_baseline leg).  Same stages and arithmetic
-as fmcw_oracle.process (window -> range FFT -> corner turn -> Doppler window -> Doppler FFT
--> |X| -> 1-D OS-CFAR 16/4 in its counting form), but fp32 and vectorised over frames, with
-scipy.fft's pocketfft using `workers` threads.  The reference itself has no software path
-(VHDL + Xilinx FFT IP), so this "port" is the CPU number the GPU is
-reported beside.
+TEST/BENCH INFRASTRUCTURE ONLY (bench.py's cpu_baseline leg).  The reference has no software
+path (VHDL + Xilinx FFT IP), so the CPU number the GPU is reported beside is
+the build's own restatement (SURVEY.md 8d "CPU baseline"):
+
+  C backend   oracle/fmcw_cpu.c (OpenMP, fp32 Stockham FFT, the oracle's CFAR definitions):
+              single-core and all-core frames/s, median of >= 20 timed runs after a warm-up.
+  NumPy port  process_frames below (scipy.fft with `workers` threads, 1-D CFAR in counting
+              form): reported beside it for continuity with round 1.
+
+Thread count: every CPU this process may run on (os.sched_getaffinity), capped by
+OMP_NUM_THREADS when the environment sets it (the GPU box grants a job 16 CPUs and sets
+OMP_NUM_THREADS=16; nproc there counts the whole machine).  All of it is reported.
 """
 from __future__ import annotations
 
 import os
+import statistics
 import time
 
 import numpy as np
@@ -38,10 +45,48 @@ def process_frames(cube: np.ndarray, workers: int, cfar=O.Cfar1D()):
     return mag, int(det.sum())
 
 
+def threads_allowed() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, n)
+
+
+def _median_runs(fn, runs: int, budget_s: float):
+    fn()                                   # warm-up (pages, plans, thread pool)
+    times = []
+    t_end = time.perf_counter() + budget_s
+    while len(times) < runs or (time.perf_counter() < t_end and len(times) < 4 * runs):
+        t0 = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - t0)
+        if len(times) >= runs and time.perf_counter() > t_end:
+            break
+    return statistics.median(times), len(times)
+
+
+def measure_c(cube: np.ndarray, cfar, runs: int = 20, budget_s: float = 8.0) -> dict:
+    """C backend on `cube` [F][rx][chirp][sample]: median seconds per run -> frames/s, at one
+    thread and at threads_allowed() threads."""
+    import cpu_backend as CB
+    F = cube.shape[0]
+    info = CB.host_info()
+    nt = threads_allowed()
+    out = {"frames_per_run": F, "threads_all": nt, **info}
+    for key, th in (("single_core", 1), ("all_core", nt)):
+        med, n = _median_runs(lambda: CB.process(cube, cfar, threads=th, want_map=False), runs, budget_s)
+        out[key] = {"frames_per_s": F / med, "median_s": med, "runs": n, "threads": th}
+    return out
+
+
 def measure(ns: int, nc: int, make_frames, target_s: float = 12.0, max_frames: int = 2048,
             batch: int = 8, workers: int | None = None):
-    """Time process_frames on batches of `batch` frames until ~target_s of CPU work."""
-    workers = workers or min(16, os.cpu_count() or 1)
+    """NumPy port: time process_frames on batches of `batch` frames until ~target_s."""
+    workers = workers or threads_allowed()
     frames = make_frames(batch)
     process_frames(frames[:1], workers)  # warm-up (plans, pages)
     done, t0 = 0, time.perf_counter()

@@ -323,6 +323,86 @@ def cfar_os2d(mag: np.ndarray, p: Cfar2D = Cfar2D()):
     return det, thr_out
 
 
+# ---------------------------------------------------------------------------
+# RTL-compat CFAR arithmetic (integer).  Cells are the 17-bit unsigned
+# CFAR input words (DATA_WIDTH 17, os_cfar.vhd:13, os_cfar_2d.vhd:11).
+# ---------------------------------------------------------------------------
+Q17_MAX = (1 << 17) - 1
+
+
+def q17(mag: np.ndarray) -> np.ndarray:
+    """Map cells -> the 17-bit CFAR word: min(floor(max(x, 0)), 2^17 - 1), int64."""
+    m = np.floor(np.maximum(np.asarray(mag, np.float64), 0.0))
+    return np.minimum(m, Q17_MAX).astype(np.int64)
+
+
+def cfar_os1d_rtl(mag: np.ndarray, p: Cfar1D = Cfar1D()):
+    """rtl/old/os_cfar.vhd:98-144 in integers: refs sorted (bubble sort :117-125),
+    threshold = resize(refs[RANK] * SCALING_MULT / SCALING_DIV, DATA_WIDTH) (:132), i.e. the
+    product taken mod 2^17, detect cut > threshold (:137).  alpha = SCALING_MULT (DIV = 1).
+    Circular along Doppler (build spec).  Returns (det, threshold int64)."""
+    assert float(p.alpha).is_integer()
+    m = q17(mag)
+    offs = [-(p.guard + 1 + i) for i in range(p.ref)] + [p.guard + 1 + i for i in range(p.ref)]
+    refs = np.sort(np.stack([np.roll(m, -o, axis=-1) for o in offs]), axis=0)
+    thr = (refs[p.rank] * int(p.alpha)) % (1 << 17)
+    return m > thr, thr
+
+
+def cfar_os2d_rtl(mag: np.ndarray, p: Cfar2D = Cfar2D()):
+    """rtl/src/os_cfar_2d.vhd:152-217 in integers: exact sum of the refs (:163), mean =
+    floor(sum / N_REF) (:189), brackets with the 17-bit add mean + (mean >> 1) (:193, wraps mod
+    2^17) and mean >> 1 (:195), threshold = ranked * scale at full width (:204), detect
+    cut > threshold (:213).  Doppler circular, range edges as cfar_os2d."""
+    m = q17(mag)
+    nr, nd = m.shape
+    hr = p.ref_range + p.guard_range
+    offs = cfar2d_offsets(p)
+    det = np.zeros((nr, nd), bool)
+    thr_out = np.zeros((nr, nd), np.int64)
+    if nr < 2 * hr + 1:
+        return det, thr_out
+    rows = np.arange(hr, nr - hr)
+    refs = np.stack([np.roll(m[rows + dr], -dd, axis=-1) for (dr, dd) in offs])
+    mean = refs.sum(axis=0) // len(offs)
+    ranked = np.sort(refs, axis=0)[p.rank]
+    if p.scale_override:
+        scale = np.full(ranked.shape, p.scale_override, np.int64)
+    else:
+        hi = (mean + (mean >> 1)) % (1 << 17)
+        lo = mean >> 1
+        scale = np.where(ranked > hi, p.scale_max, np.where(ranked < lo, p.scale_min, p.scale_nom))
+    thr = ranked * scale
+    det[rows] = m[rows] > thr
+    thr_out[rows] = thr
+    return det, thr_out
+
+
+def detections_rtl(det: np.ndarray, mag: np.ndarray, thr: np.ndarray, frame: int = 0) -> np.ndarray:
+    """Detection records of the compat CFAR: mag = the 17-bit cut word, threshold = T."""
+    return detections(det, q17(mag).astype(np.float32), np.asarray(thr).astype(np.float32), frame)
+
+
+def mti_spectrum_rtl(spec_rc: np.ndarray, mode: int) -> np.ndarray:
+    """FMCW_COMPAT_MTI on a (scaled) corner-turned spectrum [..., range, chirp]: each
+    component rounded half-to-even and saturated to int16 (the FFT IP's 16-bit output word),
+    then mti_rtl_int16 along slow time per range bin (doppler_notch.vhd:67-102)."""
+    x = np.asarray(spec_rc)
+
+    def one(v):  # mti_rtl_int16 along the last axis, all range bins at once
+        v = np.clip(np.rint(v), -32768, 32767).astype(np.int64)
+        v1 = np.zeros_like(v)
+        v1[..., 1:] = v[..., :-1]
+        if mode == 2:
+            y = v - v1
+        else:
+            v2 = np.zeros_like(v)
+            v2[..., 2:] = v[..., :-2]
+            y = v - 2 * v1 + v2
+        return np.clip(y, -32768, 32767)
+    return one(x.real) + 1j * one(x.imag)
+
+
 DET_DTYPE = np.dtype([("frame", "<u4"), ("range", "<u2"), ("doppler", "<u2"),
                       ("mag", "<f4"), ("threshold", "<f4")])
 
@@ -346,7 +426,7 @@ def detections(det: np.ndarray, mag: np.ndarray, thr: np.ndarray, frame: int = 0
 
 
 def process(cube: np.ndarray, cfar=None, window: bool = True, mti_mode: int = 0,
-            q15_rtl: bool = False):
+            q15_rtl: bool = False, range_shift: int = 0, mti_rtl: bool = False):
     """Full hot path for one frame.
 
     cube: [rx, chirp, sample] (or [chirp, sample]) complex.  Returns dict with the
@@ -366,7 +446,12 @@ def process(cube: np.ndarray, cfar=None, window: bool = True, mti_mode: int = 0,
         if c.ndim == 2:
             c = c[None]
         spec = range_ct(c, window)
-    rd = doppler_fft(mti(spec, mti_mode), window)  # [rx, range, doppler]
+    spec = spec * 2.0 ** -range_shift            # the IP's fixed scaling schedule (exact)
+    if mti_rtl:
+        spec = mti_spectrum_rtl(spec, mti_mode)
+    else:
+        spec = mti(spec, mti_mode)
+    rd = doppler_fft(spec, window)  # [rx, range, doppler]
     mag = magnitude(rd, rx_axis=0)
     mag32 = mag.astype(np.float32)
     if cfar is None:

@@ -43,7 +43,7 @@ def test_gfx950_code_object_present(lib_built):
 
 def test_struct_layouts():
     assert C.sizeof(L.FmcwDet) == 16
-    assert C.sizeof(L.FmcwConfig) == 25 * 4
+    assert C.sizeof(L.FmcwConfig) == 27 * 4          # ABI 2 (fmcw.h FMCW_ABI_VERSION)
     assert L.FmcwDet.range.offset == 4 and L.FmcwDet.mag.offset == 8
 
 
@@ -57,7 +57,8 @@ def test_defaults_mirror_radar_core(lib_built):
             cfg.cfar2d_scale_max, cfg.cfar2d_scale_override) == (75, 2, 4, 6, 0)
     assert (cfg.cfar1d_ref, cfg.cfar1d_guard, cfg.cfar1d_rank) == (8, 2, 12)
     assert cfg.cfar1d_alpha == 4.0
-    assert lib_built.fmcw_abi_version() == 1
+    assert lib_built.fmcw_abi_version() == 2
+    assert (cfg.compat_rtl, cfg.range_shift) == (0, 0)
     assert b"gfx950" in lib_built.fmcw_version()
 
 
@@ -69,6 +70,10 @@ def test_defaults_mirror_radar_core(lib_built):
     ("mti_mode", 1, b"mti_mode"), ("window", 3, b"window"),
     ("window", 2, b"in_dtype I16"),         # Q15_RTL windows int16 words only (default in f32)
     ("cfar2d_ref_doppler", 12, b"2-D CFAR"), ("max_frames", 0, b"max_frames"),
+    ("cfar2d_rank_pct", 101, b"rank_pct"), ("cfar2d_rank_pct", 0xFFFFFFFF, b"rank_pct"),
+    ("cfar2d_ref_range", 1 << 30, b"extents"),
+    ("compat_rtl", 4, b"compat_rtl"), ("compat_rtl", 2, b"compat MTI"),   # MTI compat needs MTI on
+    ("range_shift", 14, b"range_shift"),
 ])
 def test_create_rejects_bad_config(lib_built, field, value, msg):
     cfg = L.default_config()
@@ -78,6 +83,31 @@ def test_create_rejects_bad_config(lib_built, field, value, msg):
     assert rc == L.FMCW_EINVAL
     assert msg in lib_built.fmcw_last_error()
     assert not h.value
+
+
+def test_compat_cfar_needs_integer_alpha(lib_built):
+    cfg = L.default_config()
+    cfg.cfar_kind, cfg.compat_rtl, cfg.cfar1d_alpha = L.CFAR_OS1D, L.COMPAT_CFAR, 2.5
+    h = C.c_void_p()
+    assert lib_built.fmcw_create(C.byref(cfg), C.byref(h)) == L.FMCW_EINVAL
+    assert b"SCALING_MULT" in lib_built.fmcw_last_error()
+
+
+def test_gather_argument_checks(lib_built):
+    assert lib_built.fmcw_comm_create(None, 1, 0, 0, None) == L.FMCW_EINVAL
+    idbuf = C.create_string_buffer(L.COMM_ID_BYTES)
+    h = C.c_void_p()
+    assert lib_built.fmcw_comm_create(idbuf, 2, 5, 0, C.byref(h)) == L.FMCW_EINVAL
+    assert lib_built.fmcw_gather_dets(None, None, None, 1, 0, None, None, 0, None) == L.FMCW_EINVAL
+    assert lib_built.fmcw_comm_destroy(None) == L.FMCW_OK
+
+
+def test_integration_doc_struct_sizes():
+    """INTEGRATION.md's reference-side bindings allocate fmcw_config at its real size."""
+    doc = (L.PKG_ROOT.parent / "INTEGRATION.md").read_text()
+    words = C.sizeof(L.FmcwConfig) // 4
+    assert f"(C.c_uint32 * {words})()" in doc
+    assert f"Buffer.alloc({C.sizeof(L.FmcwConfig)})" in doc
 
 
 def test_create_without_device_fails_cleanly(lib_built):

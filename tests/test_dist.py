@@ -72,3 +72,38 @@ def test_shard_frames_partition():
             blocks = [shard_frames(F, G, r) for r in range(G)]
             assert blocks[0][0] == 0 and blocks[-1][1] == F
             assert all(blocks[i][1] == blocks[i + 1][0] for i in range(G - 1))
+
+
+def _worker_overfull(rank, world, port, q):
+    import warnings
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rec = torch.arange(6 * 4, dtype=torch.int32).reshape(6, 4)
+        # fmcw.h n_dets_dev: [0] found (beyond this 6-row buffer on rank 0), [1] lost in scratch
+        nd = torch.tensor([9, 0] if rank == 0 else [2, 3], dtype=torch.int32)
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            allr, counts = gather_detections(rec, nd, frame_offset=0)
+        q.put((rank, counts, allr.shape[0], len(w)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_clamps_to_the_buffer_and_warns():
+    """a count beyond the buffer (or library-side losses) must neither crash the
+    gather nor pass silently."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_overfull, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, counts, total, n_warn in res:
+        assert counts == [6, 2] and total == 8
+        assert n_warn == 1            # each rank warns about its own incomplete list

@@ -164,3 +164,75 @@ def test_cfar_defaults_match_reference_generics():
     assert len(O.cfar2d_offsets(p)) == 128
     q = O.Cfar1D()
     assert 2 * q.ref == 16 and q.rank == 12 and q.alpha == 4.0
+
+
+def test_tb_radar_core_v3_stimulus_invariants():
+    """The exact rtl/old/tb_radar_core.vhd:86-141 stimulus (IEEE UNIFORM noise, seeds 1/1, two
+    CPIs) through the oracle: both CPIs put their energy in the rows data/radar_output.txt
+    carries (99-101, 499-501), with Doppler peaks at natural bins 5 and 118."""
+    from fmcw import synth
+    cpis = synth.tb_radar_core_v3_cpis()
+    assert cpis.shape == (2, 128, 1024, 2) and cpis.dtype == np.int16
+    top = set(np.load(GOLDEN / "radar_output_profile.npz")["top_rows"].tolist())
+    for k in range(2):
+        x = cpis[k].astype(np.float64)
+        mag = O.process(x[..., 0] + 1j * x[..., 1], None)["mag"]
+        assert set(np.argsort(-mag.sum(axis=1))[:6].tolist()) == top
+        assert int(np.argmax(mag[100])) == 5 and int(np.argmax(mag[500])) == 118
+    # noise stays inside +-20 of the two tones (VHDL integer() rounding, no saturation)
+    n = np.arange(1024)[None, :]
+    c = np.arange(128)[:, None]
+    tone = 8000 * np.exp(2j * np.pi * (100 * n / 1024 + 5 * c / 128)) + \
+        5000 * np.exp(2j * np.pi * (500 * n / 1024 - 10 * c / 128))
+    x = cpis[0].astype(np.float64)
+    assert np.abs(x[..., 0] - tone.real).max() <= 20.5 and np.abs(x[..., 1] - tone.imag).max() <= 20.5
+
+
+def test_ieee_uniform_recurrence():
+    """MATH_REAL.UNIFORM: L'Ecuyer's two MLCGs (40014 mod 2147483563, 40692 mod 2147483399) in
+    (0, 1); Schrage's decomposition used by the VHDL body equals the direct product."""
+    from fmcw import synth
+    u, s1, s2 = synth.ieee_uniform(1, 1, 1000)
+    assert np.all((u > 0) & (u < 1)) and abs(u.mean() - 0.5) < 0.05
+    assert (s1, s2) == (pow(40014, 1000, 2147483563), pow(40692, 1000, 2147483399))
+    t1 = 123456789
+    k = t1 // 53668
+    schrage = 40014 * (t1 - k * 53668) - k * 12211
+    assert (schrage + 2147483563 if schrage < 0 else schrage) == (40014 * t1) % 2147483563
+
+
+def test_rtl_compat_cfar_semantics():
+    """RTL-compat CFAR restatements (os_cfar.vhd:132, os_cfar_2d.vhd:189-213): 17-bit cells,
+    the 1-D threshold wraps mod 2^17, the 2-D mean is floor(sum / 128) and its 17-bit bracket
+    add wraps, threshold at full width."""
+    # 1-D: a CUT of 30000 between refs of 40000 detects only because 4 * 40000 wraps to 28928
+    m = np.full((1, 64), 40000.0)
+    m[0, 20] = 30000.0
+    det, thr = O.cfar_os1d_rtl(m, O.Cfar1D())
+    assert det[0, 20] and thr[0, 20] == (4 * 40000) % (1 << 17) == 28928
+    assert not O.cfar_os1d(m.astype(np.float32), O.Cfar1D())[0][0, 20]
+    # quantisation: negatives -> 0, fractions floored, saturation at 2^17 - 1
+    np.testing.assert_array_equal(O.q17(np.array([-3.0, 2.9, 2.0 ** 20])), [0, 2, (1 << 17) - 1])
+    # 2-D: integer cells give the float definition's result wherever the brackets agree; the
+    # tb_os_cfar_2d map (integers) finds both targets in compat arithmetic too
+    z = np.load(GOLDEN / "tb_cfar2d.npz")
+    rr, gr, rd, gd = z["params"].tolist()
+    p = O.Cfar2D(ref_range=rr, guard_range=gr, ref_doppler=rd, guard_doppler=gd)
+    det, thr = O.cfar_os2d_rtl(z["map"], p)
+    assert det[30, 16] and det[50, 8]
+    # the 17-bit bracket add: mean 100000 -> hi = 150000 mod 2^17 = 18928 < ranked -> scale_max
+    mm = np.full((16, 32), 100000.0)
+    det, thr = O.cfar_os2d_rtl(mm, O.Cfar2D())
+    assert thr[8, 0] == 100000 * 6
+    det_f, thr_f = O.cfar_os2d(mm.astype(np.float32), O.Cfar2D())
+    assert thr_f[8, 0] == 100000 * 4                  # the float spec has no wrap: scale_nom
+
+
+def test_mti_spectrum_rtl():
+    """FMCW_COMPAT_MTI restatement: spectrum rounded half-to-even and saturated to int16, then
+    the saturating canceller (doppler_notch.vhd:67-93)."""
+    x = np.array([[0.5, 1.5, 2.5, 40000.0, -40000.0, 3.0]]) + 0j
+    y = O.mti_spectrum_rtl(x, 2)
+    np.testing.assert_array_equal(y.real[0], [0, 2, 0, 32765, -32768, 32767])
+    y3 = O.mti_spectrum_rtl(x, 3)
+    np.testing.assert_array_equal(y3.real[0], [0, 2, -2, 32765, -32768, 32767])

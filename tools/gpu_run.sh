@@ -20,8 +20,9 @@ run() {  # name limit cmd...
 for s in "$@"; do
   case $s in
     smoke) run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
-    tests_all) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -v -x --timeout 170 --timeout-method thread -p no:cacheprovider ;;
+    tests_all) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 170 --timeout-method thread -p no:cacheprovider ;;
+    tests_r02) run pytest_gpu_r02 600 python -u -m pytest tests/test_gpu_r02.py -m gpu -v --timeout 170 --timeout-method thread -p no:cacheprovider ;;
     bench) run bench 600 python bench.py --steps 10 --warmup 3 ;;
     bench_c*) run "$s" 600 python bench.py --workload "${s#bench_}" --steps 10 --warmup 3 --no-cpu-baseline ;;
     prof) run rocprof_stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
