@@ -31,6 +31,7 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "fpga-fmcw-radar-processor_amd"))
 
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PMC_FILE = "pmc_r02.json"  # per-launch HBM bytes from rocprofv3 FETCH_SIZE / WRITE_SIZE passes
 
 WORKLOADS = {
     "c2": dict(ns=1024, nc=256, nrx=1, dtype="f32", cfar="os1d", frames=1024, recipe="two_targets",
@@ -214,21 +215,37 @@ def main():
         kern["k_range"]["GBps_algorithmic"] = bytes_range / (ms_r * 1e-3) / 1e9
     if ms_d:
         kern["k_doppler"]["GBps_algorithmic"] = bytes_dopp / (ms_d * 1e-3) / 1e9
-    achieved = bytes_range / (ms_r * 1e-3) / 1e9 if ms_r else None
-    traffic = None
-    pmc_file = REPO / "profiles" / "pmc_r01.json"
+    ms_f, n_f = kt["k_fused"]
+    pmc = {}
+    pmc_file = REPO / "profiles" / PMC_FILE
     if pmc_file.exists():
         try:
             pmc = json.loads(pmc_file.read_text())
-            if pmc.get("workload") == args.workload and pmc.get("frames_per_launch") == F // max(1, n_r // args.steps):
-                traffic = pmc.get("k_range_bytes_per_launch")
         except Exception:
-            traffic = None
-    roofline = {"kernel": "k_range (window + range FFT + corner turn)", "bound": "hbm",
-                "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None, "traffic": traffic,
-                "bytes_per_launch": bytes_range // max(1, n_r),
-                "avg_launch_ms": round(ms_r / n_r, 5) if n_r else None}
+            pmc = {}
+    if n_f:
+        # fused K1 + K2: the compulsory bytes (cube in, map out) per launch of the whole batch
+        bytes_fused = F * args.steps * (px * b_in + ns * nc * 4)
+        kern["k_fused"]["GBps_algorithmic"] = bytes_fused / (ms_f * 1e-3) / 1e9
+        achieved = bytes_fused / (ms_f * 1e-3) / 1e9
+        traffic = None
+        if pmc.get("workload") == args.workload and pmc.get("frames_per_launch") == F // max(1, n_f // args.steps):
+            traffic = pmc.get("k_fused_bytes_per_launch")
+        roofline = {"kernel": "k_fused (window + range FFT + corner turn in L2 + Doppler FFT + |X| + map + 1-D CFAR)",
+                    "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                    "bytes_per_launch": bytes_fused // max(1, n_f),
+                    "avg_launch_ms": round(ms_f / n_f, 5)}
+    else:
+        achieved = bytes_range / (ms_r * 1e-3) / 1e9 if ms_r else None
+        traffic = None
+        if pmc.get("workload") == args.workload and pmc.get("frames_per_launch") == F // max(1, n_r // args.steps):
+            traffic = pmc.get("k_range_bytes_per_launch")
+        roofline = {"kernel": "k_range (window + range FFT + corner turn)", "bound": "hbm",
+                    "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None, "traffic": traffic,
+                    "bytes_per_launch": bytes_range // max(1, n_r),
+                    "avg_launch_ms": round(ms_r / n_r, 5) if n_r else None}
     e2e_bytes = F * (px * b_in + ns * nc * 4) + 16 * n_det_step
 
     # H2D-inclusive rate: the cube streamed from pinned host memory inside each step (copy of
@@ -326,6 +343,8 @@ def main():
                    "detection_gather": gather_kind if gather else "none (single GPU)",
                    "parallelism": f"frame-sharded x{world}"},
         "e2e_GBps_algorithmic": round(e2e_bytes * args.steps * world / elapsed / 1e9, 1),
+        "e2e_frac_of_peak": round(e2e_bytes * args.steps / elapsed / 1e9 / HBM_PEAK_GBPS, 4),
+        "fused_path": bool(core.info("fused")),
         "detections_per_step": n_det_step,
         "roofline": roofline,
         "kernels": kern,

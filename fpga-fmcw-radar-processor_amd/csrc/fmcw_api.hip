@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -84,12 +85,27 @@ struct fmcw_handle {
   // grid sizes
   int grid_range = 0, grid_doppler = 0, grid_cfar = 0;
   size_t cfar2d_smem = 0;
+  // two-stream chunk pipeline (K1 of chunk c + 1 beside K2 of chunk c, fmcw_enqueue)
+  int pipe_nb = 0;                      // intermediate buffers in the ring (0 = serial chunks)
+  float2* inter_b[3] = {nullptr, nullptr, nullptr};
+  float* lin_b[3] = {nullptr, nullptr, nullptr};
+  hipStream_t ps[2] = {nullptr, nullptr};
+  hipEvent_t ev_k1[3] = {}, ev_free[3] = {}, ev_fork = nullptr, ev_join = nullptr;
+  // fused K1 + K2 (fused.hpp)
+  bool fused_ok = false;
+  void (*fused_fn)(FusedArgs) = nullptr;
+  int fused_per_xcd = 0, fused_na = 0, fused_nb = 0;
+  float2* fused_spec = nullptr;  // 8 frame spectra, one per XCD (L2-resident)
+  uint32_t* fused_ctl = nullptr;
+  uint64_t* fused_trace = nullptr;  // FMCW_FUSED_TRACE=1: phase timestamps of every launch
+  int64_t fused_fallbacks = 0;
+  bool fused_used_last = false;  // the last fmcw_enqueue ran the fused kernel
   // profiling
   bool profiling = false;
   std::vector<PendingEvent> pending;
   std::vector<hipEvent_t> free_events;
-  double ms[FMCW_K_COUNT] = {0, 0, 0, 0};
-  uint64_t launches[FMCW_K_COUNT] = {0, 0, 0, 0};
+  double ms[FMCW_K_COUNT] = {};
+  uint64_t launches[FMCW_K_COUNT] = {};
 };
 
 namespace {
@@ -169,6 +185,30 @@ Cfar2Info cfar2_info(uint32_t nc, int hd = 0, int gd = 0) {
 #undef C_
   }
   return {nullptr, 0};
+}
+
+// fused K1 + K2 instantiations: the reference core (1024 x 128), BASELINE config 2 (1024 x 256)
+// and two more shapes with 256-thread range and Doppler workgroups and <= 2 MiB spectra
+using FusedFn = void (*)(FusedArgs);
+template <int N, int NC>
+FusedFn fused_fn_t(int dtype) {
+  switch (dtype) {
+    case FMCW_IN_F32: return k_fused<N, NC, LoadF32>;
+    case FMCW_IN_F16: return k_fused<N, NC, LoadF16>;
+    case FMCW_IN_I16: return k_fused<N, NC, LoadI16>;
+  }
+  return nullptr;
+}
+struct FusedInfo {
+  FusedFn fn;
+  int upf, wtpf;
+};
+FusedInfo fused_info(uint32_t n, uint32_t nc, int dtype) {
+#define F_(N, NC) \
+  if (n == N && nc == NC) return {fused_fn_t<N, NC>(dtype), FusedGeom<N, NC>::UPF, FusedGeom<N, NC>::WTPF};
+  F_(1024, 256) F_(1024, 128) F_(512, 256) F_(2048, 128)
+#undef F_
+  return {nullptr, 0, 0};
 }
 
 // 2-D CFAR derived parameters
@@ -393,7 +433,8 @@ int launch_det_finish(fmcw_handle* h, size_t n_frames, fmcw_det* dets, size_t de
   ProfScope ps(h, FMCW_K_COMPACT, s);
   hipLaunchKernelGGL(k_det_scan_blocks, dim3(nb), dim3(1024), 0, s, h->wg_count, h->wg_off, n, h->block_sum);
   hipLaunchKernelGGL(k_det_scan_top, dim3(1), dim3(1024), 0, s, h->block_sum, nb, n_dets_dev,
-                     (const uint32_t*)(h->counter + 1));
+                     (const uint32_t*)(h->counter + 1),
+                     (const uint32_t*)(h->fused_used_last ? h->fused_ctl + FusedCtl::kErr : nullptr));
   int rc = check_launch("k_det_scan");
   if (rc) return rc;
   if (dets && det_cap) {
@@ -443,6 +484,73 @@ int ensure_stage(T** p, size_t* have, size_t need_bytes, const char* what) {
 }
 
 }  // namespace
+
+// Decide whether this handle runs the fused K1 + K2 kernel and, if so, verify on the device
+// that its persistent grid lands as the kernel needs: exactly per_xcd workgroups on every XCD,
+// all co-resident (a census launch of the kernel itself: join, wait for the group, exit).
+// Placement is never assumed -- a device or runtime that places differently keeps K1 + K2.
+void setup_fused(fmcw_handle* h) {
+  const fmcw_config& c = h->cfg;
+  // opt-in (FMCW_FUSED=1): measured slower than the K1/K2 pipeline at config 2
+  const char* env = std::getenv("FMCW_FUSED");
+  if (!env || env[0] != '1') return;
+  if (c.n_rx != 1 || c.mti_mode != FMCW_MTI_OFF || c.window == FMCW_WIN_Q15_RTL) return;
+  if (h->n_cu % 8 != 0) return;
+  const FusedInfo fi = fused_info(c.n_range, c.n_doppler, c.in_dtype);
+  if (!fi.fn) return;
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(fi.fn), 256, 0) !=
+          hipSuccess ||
+      occ < 1) {
+    (void)hipGetLastError();
+    return;
+  }
+  occ = std::min(occ, 4);
+  const int per_xcd = occ * h->n_cu / 8;
+  // Doppler workgroups (4 waves, at most one wave tile each per frame): 3/4 of the group by
+  // default (FMCW_FUSED_NB overrides), at least enough to cover a frame's wave tiles
+  const char* nbs = std::getenv("FMCW_FUSED_NB");
+  int nb = nbs ? std::atoi(nbs) : per_xcd * 3 / 4;
+  nb = std::max(nb, (fi.wtpf + 3) / 4);
+  const int na = std::min(per_xcd - nb, fi.upf);  // every range workgroup has a unit per frame
+  if (na < 8) return;
+  const size_t spec_bytes = 8 * kRing * (size_t)c.n_range * c.n_doppler * sizeof(float2);
+  if (hipMalloc(reinterpret_cast<void**>(&h->fused_spec), spec_bytes) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&h->fused_ctl), FusedCtl::kWords * 4) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  FusedArgs a{};
+  a.ctl = h->fused_ctl;
+  a.per_xcd = per_xcd;
+  a.n_a = na;
+  a.n_b = nb;
+  a.census = 1;
+  a.spin_limit = 20000;
+  std::vector<uint32_t> ctl(FusedCtl::kWords, 0);
+  if (hipMemset(h->fused_ctl, 0, FusedCtl::kWords * 4) != hipSuccess) return;
+  hipLaunchKernelGGL(fi.fn, dim3(8 * per_xcd), dim3(256), 0, 0, a);
+  if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(ctl.data(), h->fused_ctl, FusedCtl::kWords * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  if (ctl[FusedCtl::kErr] != 0) return;
+  for (int x = 0; x < 8; ++x)
+    if (ctl[FusedCtl::join(x)] != (uint32_t)per_xcd) return;
+  if (std::getenv("FMCW_FUSED_VERBOSE"))
+    std::fprintf(stderr, "fmcw: fused kernel on, %d workgroups per XCD (%d range, %d Doppler)\n", per_xcd, na, nb);
+  const char* tr = std::getenv("FMCW_FUSED_TRACE");
+  if (tr && tr[0] == '1' && hipMalloc(reinterpret_cast<void**>(&h->fused_trace), 8 * kTraceFrames * 8 * 8) != hipSuccess) {
+    (void)hipGetLastError();
+    h->fused_trace = nullptr;
+  }
+  h->fused_fn = fi.fn;
+  h->fused_per_xcd = per_xcd;
+  h->fused_na = na;
+  h->fused_nb = nb;
+  h->fused_ok = true;
+}
 
 // the thread-local fmcw_last_error() message, for the other translation units of the library
 int fmcw_internal_fail(int code, const char* msg) { return fail(code, "%s", msg); }
@@ -511,7 +619,17 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   h->lgT = __builtin_ctz(ri.T);
   h->lgRB = __builtin_ctz(ri.RB);
   const size_t frame_inter = (size_t)c.n_rx * c.n_range * c.n_doppler * sizeof(float2);
-  if (c.chunk_frames) {
+  // two-stream pipeline of chunks (FMCW_PIPE=1): ring of FMCW_PIPE_BUFS intermediate buffers of
+  // FMCW_PIPE_CHUNK frames, sized so the ring stays in the 256 MiB Infinity Cache
+  const char* pe = std::getenv("FMCW_PIPE");
+  const bool pipe = pe && pe[0] == '1';
+  if (pipe) {
+    const char* pc = std::getenv("FMCW_PIPE_CHUNK");
+    const char* pb = std::getenv("FMCW_PIPE_BUFS");
+    h->pipe_nb = std::max(2, std::min(3, pb ? std::atoi(pb) : 2));
+    const size_t want = pc ? (size_t)std::max(1, std::atoi(pc)) : std::max<size_t>(1, (64u << 20) / frame_inter);
+    h->chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(c.max_frames, want));
+  } else if (c.chunk_frames) {
     h->chunk = std::min<uint32_t>(c.chunk_frames, c.max_frames);
   } else {
     // ~256 MiB of corner-turned intermediate per chunk: measured on config 2, 32 -> 128 frames
@@ -534,6 +652,24 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   ALLOC(h->win_d, c.n_doppler * sizeof(float));
   ALLOC(h->inter, h->chunk * frame_inter);
   if (c.cfar_kind == FMCW_CFAR_OS2D) ALLOC(h->lin_scratch, (size_t)h->chunk * c.n_range * c.n_doppler * sizeof(float));
+  if (h->pipe_nb) {
+    h->inter_b[0] = h->inter;
+    h->lin_b[0] = h->lin_scratch;
+    for (int b = 1; b < h->pipe_nb; ++b) {
+      ALLOC(h->inter_b[b], h->chunk * frame_inter);
+      if (c.cfar_kind == FMCW_CFAR_OS2D) ALLOC(h->lin_b[b], (size_t)h->chunk * c.n_range * c.n_doppler * sizeof(float));
+    }
+    for (int i = 0; i < 2; ++i)
+      if (hipStreamCreateWithFlags(&h->ps[i], hipStreamNonBlocking) != hipSuccess)
+        return cleanup(fail(FMCW_EHIP, "stream create"));
+    for (int b = 0; b < h->pipe_nb; ++b)
+      if (hipEventCreateWithFlags(&h->ev_k1[b], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&h->ev_free[b], hipEventDisableTiming) != hipSuccess)
+        return cleanup(fail(FMCW_EHIP, "event create"));
+    if (hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess)
+      return cleanup(fail(FMCW_EHIP, "event create"));
+  }
   h->n_wg_max = (size_t)c.max_frames * tiles_per_frame(h);
   {
     // Each tile owns a slot of 1/32 of its cells (a 3 % detection density, far above any
@@ -581,6 +717,7 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
       (void)hipGetLastError();
     occupancy_grid(ci.fn, 256, h->cfar2d_smem, h->n_cu, &h->grid_cfar);
   }
+  setup_fused(h);
   *out = h;
   return FMCW_OK;
 }
@@ -590,7 +727,7 @@ int fmcw_destroy(fmcw_handle* h) {
   hipSetDevice(h->cfg.device_id);
   void* ptrs[] = {h->win_r, h->win_d, h->inter, h->lin_scratch, h->det_scratch, h->counter,
                   h->n_dets_tmp, h->wg_base, h->wg_count, h->wg_off, h->block_sum,
-                  h->stage_cube, h->stage_map, h->stage_dets};
+                  h->stage_cube, h->stage_map, h->stage_dets, h->fused_spec, h->fused_ctl, h->fused_trace};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& pe : h->pending) {
@@ -598,6 +735,18 @@ int fmcw_destroy(fmcw_handle* h) {
     hipEventDestroy(pe.b);
   }
   for (auto e : h->free_events) hipEventDestroy(e);
+  for (int b = 1; b < 3; ++b) {
+    if (h->inter_b[b]) hipFree(h->inter_b[b]);
+    if (h->lin_b[b]) hipFree(h->lin_b[b]);
+  }
+  for (int b = 0; b < 3; ++b) {
+    if (h->ev_k1[b]) hipEventDestroy(h->ev_k1[b]);
+    if (h->ev_free[b]) hipEventDestroy(h->ev_free[b]);
+  }
+  if (h->ev_fork) hipEventDestroy(h->ev_fork);
+  if (h->ev_join) hipEventDestroy(h->ev_join);
+  for (int i = 0; i < 2; ++i)
+    if (h->ps[i]) hipStreamDestroy(h->ps[i]);
   delete h;
   return FMCW_OK;
 }
@@ -621,36 +770,104 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
   int rc;
   if (c.cfar_kind != FMCW_CFAR_NONE) HIP_TRY(hipMemsetAsync(h->counter, 0, 2 * sizeof(uint32_t), s));
 
-  for (size_t f0 = 0; f0 < n_frames; f0 += h->chunk) {
+  // fused K1 + K2: one persistent launch for the whole batch (the 2-D CFAR needs the whole
+  // linear map, so it runs on the fused path only when the caller asks for that map)
+  const bool fuse = h->fused_ok && (c.cfar_kind != FMCW_CFAR_OS2D || (rd_map && c.map_kind == FMCW_MAP_LINEAR));
+  h->fused_used_last = fuse;
+  if (fuse) {
+    HIP_TRY(hipMemsetAsync(h->fused_ctl, 0, FusedCtl::kWords * 4, s));
+    FusedArgs a{};
+    a.cube = cube;
+    a.spec = h->fused_spec;
+    a.win_r = h->win_r;
+    a.chirp_w = h->win_d;
+    a.lin_map = rd_map && c.map_kind == FMCW_MAP_LINEAR ? rd_map : nullptr;
+    a.db_map = rd_map && c.map_kind == FMCW_MAP_DB ? rd_map : nullptr;
+    a.ctl = h->fused_ctl;
+    a.n_frames = (int)n_frames;
+    a.frame0 = 0;
+    a.tile0 = 0;
+    a.per_xcd = h->fused_per_xcd;
+    a.n_a = h->fused_na;
+    a.n_b = h->fused_nb;
+    a.mag_mode = c.mag_mode;
+    a.census = 0;
+    a.spin_limit = 2000000;  // ~0.1-1 s of polling: only a broken group ever reaches it
+    a.cf = cf1;
+    a.sink = sink;
+    a.trace = h->fused_trace;
+    if (h->fused_trace) HIP_TRY(hipMemsetAsync(h->fused_trace, 0, 8 * kTraceFrames * 8 * 8, s));
+    {
+      ProfScope ps(h, FMCW_K_FUSED, s);
+      hipLaunchKernelGGL(h->fused_fn, dim3(8 * h->fused_per_xcd), dim3(256), 0, s, a);
+      if ((rc = check_launch("k_fused"))) return rc;
+    }
+    if (c.cfar_kind == FMCW_CFAR_OS2D)
+      for (size_t f0 = 0; f0 < n_frames; f0 += h->chunk) {
+        const int nf = (int)std::min<size_t>(h->chunk, n_frames - f0);
+        if ((rc = launch_cfar(h, rd_map + f0 * frame_px, nf, (int)f0, s))) return rc;
+      }
+    if (c.cfar_kind != FMCW_CFAR_NONE) return launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, s);
+    return FMCW_OK;
+  }
+
+  // Chunks of h->chunk frames: K1 -> intermediate -> K2 (+ K3).  With the two-stream pipeline
+  // (h->pipe_nb buffers) chunk c's K1 runs on ps[0] beside chunk c - 1's K2 on ps[1]; buffer b
+  // is rewritten by K1 only after the K2 that read it (ev_free[b]).  Fork from / join to the
+  // caller's stream with events, so the call stays stream-ordered (and graph-capturable).
+  const size_t n_chunks = (n_frames + h->chunk - 1) / h->chunk;
+  const bool piped = h->pipe_nb > 0 && n_chunks > 1;
+  hipStream_t sa = s, sb = s;
+  if (piped) {
+    sa = h->ps[0];
+    sb = h->ps[1];
+    HIP_TRY(hipEventRecord(h->ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(sa, h->ev_fork, 0));
+    HIP_TRY(hipStreamWaitEvent(sb, h->ev_fork, 0));
+  }
+  for (size_t ci = 0; ci < n_chunks; ++ci) {
+    const size_t f0 = ci * h->chunk;
     const int nf = (int)std::min<size_t>(h->chunk, n_frames - f0);
     const void* src = static_cast<const char*>(cube) + f0 * in_frame_bytes;
+    const int b = piped ? (int)(ci % h->pipe_nb) : 0;
+    float2* inter = piped ? h->inter_b[b] : h->inter;
+    if (piped && ci >= (size_t)h->pipe_nb) HIP_TRY(hipStreamWaitEvent(sa, h->ev_free[b], 0));
     {
       const int n_groups = nf * (int)c.n_rx * (int)(c.n_doppler / ri.T);
-      ProfScope ps(h, FMCW_K_RANGE, s);
+      ProfScope ps(h, FMCW_K_RANGE, sa);
       // MTI off: K1 applies the Doppler window too (k_doppler<NC, 0> expects it)
       const float* chirp_w = c.mti_mode == FMCW_MTI_OFF ? h->win_d : nullptr;
-      hipLaunchKernelGGL(ri.fn, dim3(std::min(n_groups, h->grid_range)), dim3(ri.NT), 0, s, src, h->inter,
+      hipLaunchKernelGGL(ri.fn, dim3(std::min(n_groups, h->grid_range)), dim3(ri.NT), 0, sa, src, inter,
                          h->win_r, chirp_w, (int)c.n_doppler, n_groups, q15_scale(c));
       if ((rc = check_launch("k_range"))) return rc;
+    }
+    if (piped) {
+      HIP_TRY(hipEventRecord(h->ev_k1[b], sa));
+      HIP_TRY(hipStreamWaitEvent(sb, h->ev_k1[b], 0));
     }
     float* lin = nullptr;
     float* db = nullptr;
     if (rd_map && c.map_kind == FMCW_MAP_LINEAR) lin = rd_map + f0 * frame_px;
     if (rd_map && c.map_kind == FMCW_MAP_DB) db = rd_map + f0 * frame_px;
-    if (c.cfar_kind == FMCW_CFAR_OS2D && !lin) lin = h->lin_scratch;
+    if (c.cfar_kind == FMCW_CFAR_OS2D && !lin) lin = piped ? h->lin_b[b] : h->lin_scratch;
     {
       const int n_tiles = nf * (int)(c.n_range / di.WR);
       const int grid = std::min((n_tiles + kWavesPerBlock - 1) / kWavesPerBlock, h->grid_doppler);
-      ProfScope ps(h, FMCW_K_DOPPLER, s);
-      hipLaunchKernelGGL(di.fn, dim3(grid), dim3(di.NT), 0, s, h->inter,
+      ProfScope ps(h, FMCW_K_DOPPLER, sb);
+      hipLaunchKernelGGL(di.fn, dim3(grid), dim3(di.NT), 0, sb, inter,
                          h->win_d, (int)c.n_range, (int)c.n_rx, h->lgT, h->lgRB, n_tiles, (int)f0,
                          (int)(f0 * (c.n_range / di.WR)), lin, db, c.mag_mode,
                          (c.compat_rtl & FMCW_COMPAT_MTI) ? 1 : 0, cf1, sink);
       if ((rc = check_launch("k_doppler"))) return rc;
     }
+    if (piped) HIP_TRY(hipEventRecord(h->ev_free[b], sb));
     if (c.cfar_kind == FMCW_CFAR_OS2D) {
-      if ((rc = launch_cfar(h, lin, nf, (int)f0, s))) return rc;
+      if ((rc = launch_cfar(h, lin, nf, (int)f0, sb))) return rc;
     }
+  }
+  if (piped) {  // join: everything on ps[0] precedes ps[1]'s last K2, so ps[1] alone is enough
+    HIP_TRY(hipEventRecord(h->ev_join, sb));
+    HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));
   }
   if (c.cfar_kind != FMCW_CFAR_NONE) return launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, s);
   return FMCW_OK;
@@ -693,6 +910,17 @@ int fmcw_process(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
   if (e == hipSuccess && rd_map && d_map != rd_map)
     e = hipMemcpyAsync(rd_map, d_map, map_bytes, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess && h->fused_used_last) {
+    uint32_t ferr = 0;
+    e = hipMemcpy(&ferr, h->fused_ctl + FusedCtl::kErr, 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && ferr) {
+      // the fused launch gave up (a bounded wait expired): redo the batch on K1 + K2 and keep
+      // this handle there
+      h->fused_ok = false;
+      h->fused_fallbacks += 1;
+      return fmcw_process(h, cube, n_frames, rd_map, dets, det_cap, n_dets, stream);
+    }
+  }
   const uint32_t nd = ndd[0];
   if (e == hipSuccess && dets && d_dets != dets && nd)
     e = hipMemcpy(dets, d_dets, std::min<size_t>(nd, det_cap) * sizeof(fmcw_det), hipMemcpyDeviceToHost);
@@ -752,6 +980,7 @@ int fmcw_cfar(fmcw_handle* h, const float* map, size_t n_frames, fmcw_det* dets,
   if (n_frames < 1 || n_frames > c.max_frames) return fail(FMCW_EINVAL, "n_frames out of range");
   HIP_TRY(hipSetDevice(c.device_id));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  h->fused_used_last = false;
   HIP_TRY(hipMemsetAsync(h->counter, 0, 2 * sizeof(uint32_t), s));
   int rc = launch_cfar(h, map, (int)n_frames, 0, s);
   if (rc) return rc;
@@ -761,6 +990,25 @@ int fmcw_cfar(fmcw_handle* h, const float* map, size_t n_frames, fmcw_det* dets,
 int fmcw_set_profiling(fmcw_handle* h, int enable) {
   if (!h) return fail(FMCW_EINVAL, "null handle");
   h->profiling = enable != 0;
+  return FMCW_OK;
+}
+
+int fmcw_get_info(fmcw_handle* h, int key, int64_t* value) {
+  if (!h || !value) return fail(FMCW_EINVAL, "null argument");
+  switch (key) {
+    case FMCW_INFO_FUSED: *value = h->fused_ok ? 1 : 0; return FMCW_OK;
+    case FMCW_INFO_FUSED_GROUP: *value = h->fused_per_xcd; return FMCW_OK;
+    case FMCW_INFO_FUSED_FALLBACKS: *value = h->fused_fallbacks; return FMCW_OK;
+    case FMCW_INFO_CHUNK: *value = h->chunk; return FMCW_OK;
+  }
+  return fail(FMCW_EINVAL, "fmcw_get_info: unknown key %d", key);
+}
+
+int fmcw_get_fused_trace(fmcw_handle* h, uint64_t* out, size_t n_words) {
+  if (!h || !out) return fail(FMCW_EINVAL, "null argument");
+  if (!h->fused_trace) return fail(FMCW_EINVAL, "no fused trace (create the handle with FMCW_FUSED_TRACE=1)");
+  HIP_TRY(hipSetDevice(h->cfg.device_id));
+  HIP_TRY(hipMemcpy(out, h->fused_trace, std::min<size_t>(n_words, 8 * kTraceFrames * 8) * 8, hipMemcpyDeviceToHost));
   return FMCW_OK;
 }
 

@@ -23,6 +23,10 @@
 
 namespace fmcw {
 
+#ifndef FMCW_CFAR1D_WHOLE   // 1-D screen over the lane's whole window (1) or two 8-cell halves (0)
+#define FMCW_CFAR1D_WHOLE 1
+#endif
+
 // --------------------------------------------------------------------------------------
 // Input loaders: two consecutive complex samples -> float4 (re0, im0, re1, im1).
 // ADC word {Q[31:16], I[15:0]} (rtl/src/tb_radar_core.vhd:115-118) = little-endian short2(I,Q).
@@ -465,11 +469,56 @@ __device__ __forceinline__ void cfar1d_wave(const float* mags, uint32_t* list, i
     constexpr int NGS = REF / 4;               // groups of 4 per side
     constexpr int RO = REF + 2 * GUARD + 1;    // first right ref, relative to the first left ref
     // two halves of 8 cells (a 28-value window each) to keep the register peak low
-    constexpr int HC = CELLS / 2, WH = HC + 2 * H;
-    constexpr int NV = (WH + 3 + 3) / 4;       // 16-B reads covering the window from floor4
     const float* lb = mrow + midx(d0);
     const int need = nref - cf.rank;
     const bool one_group = need <= 4;          // the reference (rank 12 of 16): any group rejects
+#if FMCW_CFAR1D_WHOLE
+    // The lane's whole window at once: cells d0 - H .. d0 + 15 + H, group minima g[k] =
+    // min(w[k .. k+3]) over it computed once (2 mins per group), not per 8-cell half.
+    {
+      constexpr int WW = CELLS + 2 * H;        // 36 at the reference geometry
+      constexpr int O0 = floor4(-H);
+      constexpr int NV = (WW + (-H - O0) + 3) / 4;
+      float v[4 * NV];
+      load_cells<NV>(lb, O0, v);
+      float g[WW - 3];
+      {
+        float m2[WW - 1];
+#pragma unroll
+        for (int k = 0; k < WW - 1; ++k) m2[k] = fminf(v[-H - O0 + k], v[-H - O0 + k + 1]);
+#pragma unroll
+        for (int k = 0; k < WW - 3; ++k) g[k] = fminf(m2[k], m2[k + 2]);
+      }
+#pragma unroll
+      for (int i = 0; i < CELLS; ++i) {
+        const float cut = v[-O0 + i];
+        uint32_t sb;
+        if (one_group) {
+          // reject <=> alpha M >= cut for the largest group minimum M.  fma(alpha, M, -cut) < 0
+          // (exact product) survives a few cells the rounded test would reject -- never the
+          // reverse (alpha M >= cut exactly implies fl(alpha M) >= cut) -- and the exact count
+          // below decides those, so the screen stays conservative.  Sign bit = survival.
+          float M = g[i];
+#pragma unroll
+          for (int q = 1; q < NGS; ++q) M = fmaxf(M, g[i + 4 * q]);
+#pragma unroll
+          for (int q = 0; q < NGS; ++q) M = fmaxf(M, g[i + RO + 4 * q]);
+          sb = __float_as_uint(__builtin_fmaf(cf.alpha, M, -cut)) >> 31;
+        } else {
+          const uint32_t cbits = __float_as_uint(cut);
+          uint32_t nlt = 0;  // groups with alpha * min < cut
+#pragma unroll
+          for (int q = 0; q < NGS; ++q)
+            nlt += lt_bit(__float_as_uint(cf.alpha * g[i + 4 * q]), cbits) +
+                   lt_bit(__float_as_uint(cf.alpha * g[i + RO + 4 * q]), cbits);
+          sb = 4 * (2 * NGS - (int)nlt) < need ? 1u : 0u;
+        }
+        bits |= sb << i;
+      }
+    }
+#else
+    constexpr int HC = CELLS / 2, WH = HC + 2 * H;
+    constexpr int NV = (WH + 3 + 3) / 4;       // 16-B reads covering the window from floor4
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       const int ws = hh * HC - H;              // first window cell relative to d0
@@ -512,6 +561,7 @@ __device__ __forceinline__ void cfar1d_wave(const float* mags, uint32_t* list, i
         bits |= sb << (hh * HC + i);
       }
     }
+#endif
     // Exact count for the survivors only, one survivor per lane.  About 12 of a tile's 1024
     // cells survive the screen on noise + targets, but they sit in ~8 of the 16 cell
     // indices, so counting per index for the whole wave (where any lane survived) cost 8 x 16
@@ -967,6 +1017,11 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
 // --------------------------------------------------------------------------------------
 #include "cfar2d.hpp"
 
+// --------------------------------------------------------------------------------------
+// K12: K1 + K2 in one persistent launch, spectrum resident in each XCD's L2 -- see fused.hpp.
+// --------------------------------------------------------------------------------------
+#include "fused.hpp"
+
 
 // --------------------------------------------------------------------------------------
 // Detection ordering: exclusive scan over per-workgroup counts (in workgroup = (frame,
@@ -988,7 +1043,7 @@ k_det_scan_blocks(const uint32_t* __restrict__ wg_count, uint32_t* __restrict__ 
 // level 2: one workgroup scans the block sums in place (-> block offsets) and the total
 __global__ void __launch_bounds__(1024)
 k_det_scan_top(uint32_t* __restrict__ block_sum, int nb, uint32_t* __restrict__ n_dets,
-               const uint32_t* __restrict__ dropped) {
+               const uint32_t* __restrict__ dropped, const uint32_t* __restrict__ fused_err) {
   __shared__ int s_wave[1024 / 64 + 2];
   const int per = (nb + 1023) / 1024;
   const int b = threadIdx.x * per;
@@ -1005,6 +1060,8 @@ k_det_scan_top(uint32_t* __restrict__ block_sum, int nb, uint32_t* __restrict__ 
   if (threadIdx.x == 0) {
     n_dets[0] = (uint32_t)total;  // every detection found
     n_dets[1] = *dropped;         // of which not stored (handle scratch exhausted)
+    // the fused launch gave up (fused.hpp): the list is incomplete, flagged in the top bit
+    if (fused_err && *fused_err) n_dets[1] |= 0x80000000u;
   }
 }
 

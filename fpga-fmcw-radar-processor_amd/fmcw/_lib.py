@@ -25,8 +25,9 @@ CFAR_NONE, CFAR_OS1D, CFAR_OS2D = 0, 1, 2
 MTI_OFF, MTI_2PULSE, MTI_3PULSE = 0, 2, 3
 COMPAT_CFAR, COMPAT_MTI = 1, 2
 COMM_ID_BYTES = 128
-K_RANGE, K_DOPPLER, K_CFAR2D, K_COMPACT, K_COUNT = 0, 1, 2, 3, 4
-KERNEL_NAMES = ("k_range", "k_doppler", "k_cfar", "k_compact")
+K_RANGE, K_DOPPLER, K_CFAR2D, K_COMPACT, K_FUSED, K_COUNT = 0, 1, 2, 3, 4, 5
+KERNEL_NAMES = ("k_range", "k_doppler", "k_cfar", "k_compact", "k_fused")
+INFO_FUSED, INFO_FUSED_GROUP, INFO_FUSED_FALLBACKS, INFO_CHUNK = 1, 2, 3, 4
 
 STATUS_NAMES = {0: "FMCW_OK", -1: "FMCW_EINVAL", -2: "FMCW_ENOMEM", -3: "FMCW_EHIP",
                 -4: "FMCW_EDETCAP", -5: "FMCW_ENODEV"}
@@ -81,6 +82,8 @@ SIGNATURES = {
     "fmcw_magnitude": (_I, [_VP, _VP, _SZ, _I, _VP]),
     "fmcw_cfar": (_I, [_VP, _VP, _SZ, _VP, _SZ, _VP, _VP]),
     "fmcw_set_profiling": (_I, [_VP, _I]),
+    "fmcw_get_info": (_I, [_VP, _I, C.POINTER(C.c_int64)]),
+    "fmcw_get_fused_trace": (_I, [_VP, C.POINTER(C.c_uint64), _SZ]),
     "fmcw_kernel_times": (_I, [_VP, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "fmcw_reset_kernel_times": (_I, [_VP]),
     "fmcw_device_alloc": (_I, [_SZ, C.POINTER(_VP), _I]),

@@ -245,6 +245,15 @@ class RadarCore:
         L.check(self._lib.fmcw_kernel_times(self._h, ms, n))
         return {L.KERNEL_NAMES[k]: (ms[k], n[k]) for k in range(L.K_COUNT)}
 
+    def info(self, key: str) -> int:
+        """fmcw_get_info: "fused" (1 = the fused range + Doppler kernel runs), "fused_group"
+        (workgroups per XCD), "fused_fallbacks", "chunk"."""
+        k = {"fused": L.INFO_FUSED, "fused_group": L.INFO_FUSED_GROUP,
+             "fused_fallbacks": L.INFO_FUSED_FALLBACKS, "chunk": L.INFO_CHUNK}[key]
+        v = C.c_int64(0)
+        L.check(self._lib.fmcw_get_info(self._h, k, C.byref(v)))
+        return int(v.value)
+
     def reset_kernel_times(self):
         L.check(self._lib.fmcw_reset_kernel_times(self._h))
 

@@ -152,8 +152,20 @@ typedef enum {
   FMCW_K_DOPPLER = 1, /* Doppler window + FFT + magnitude (+NCI) (+1-D CFAR) + map */
   FMCW_K_CFAR2D = 2,  /* 2-D OS-CFAR */
   FMCW_K_COMPACT = 3, /* detection list ordering */
-  FMCW_K_COUNT = 4
+  FMCW_K_FUSED = 4,   /* K1 + K2 in one launch, spectrum resident in the XCD L2s */
+  FMCW_K_COUNT = 5
 } fmcw_kernel_id;
+
+/* fmcw_get_info keys.  FMCW_INFO_FUSED: 1 when fmcw_enqueue runs the fused range + Doppler
+ * kernel (one persistent launch; the corner-turned spectrum of each frame stays in one XCD's
+ * L2, the reference's on-chip corner turner, corner_turner.vhd:98-166), 0 when it runs K1 ->
+ * HBM -> K2.  Chosen at fmcw_create: one rx, MTI off, fp32 Hamming/none window, a frame
+ * spectrum <= 2 MiB, a supported (n_range, n_doppler), and a placement check of the launch on
+ * this device; environment FMCW_FUSED=0 disables it.  FMCW_INFO_FUSED_GROUP: workgroups per
+ * XCD of the fused launch.  FMCW_INFO_FUSED_FALLBACKS: fused launches that gave up (bounded
+ * waits expired) and were re-run on K1 + K2 by fmcw_process. */
+typedef enum { FMCW_INFO_FUSED = 1, FMCW_INFO_FUSED_GROUP = 2, FMCW_INFO_FUSED_FALLBACKS = 3,
+               FMCW_INFO_CHUNK = 4 } fmcw_info_key;
 
 /* Only the functions below are exported from libfmcw.so (built -fvisibility=hidden). */
 #if defined(__GNUC__)
@@ -178,8 +190,10 @@ int fmcw_destroy(fmcw_handle* h);
  *                   not written),
  *   n_dets_dev[1] = detections lost because the handle's internal detection scratch
  *                   overflowed (a tile with more than its slot that also found the shared
- *                   overflow region full).  Non-zero means the list is incomplete;
- *                   fmcw_process returns FMCW_EDETCAP in either case. */
+ *                   overflow region full); bit 31 set = the fused kernel gave up (its
+ *                   bounded inter-workgroup waits expired) and the results are incomplete.
+ *                   Non-zero means the list is incomplete; fmcw_process returns
+ *                   FMCW_EDETCAP in either case (and re-runs a failed fused batch). */
 int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_map,
                  fmcw_det* dets, size_t det_cap, uint32_t* n_dets_dev, void* stream);
 
@@ -221,6 +235,13 @@ int fmcw_gather_dets(fmcw_comm* c, const fmcw_det* dets_dev, const uint32_t* n_d
  * its stream; fmcw_kernel_times synchronises and returns, per fmcw_kernel_id, the summed
  * milliseconds and the number of launches since the last reset. */
 int fmcw_set_profiling(fmcw_handle* h, int enable);
+int fmcw_get_info(fmcw_handle* h, int key, int64_t* value);
+/* Diagnostics: with FMCW_FUSED_TRACE=1 in the environment at fmcw_create, the fused kernel
+ * records 100 MHz timestamps of its phases, [xcd 0..7][frame k 0..63][event 0..7] (events:
+ * range role first WG: frame start, past the wait for the Doppler side, after its ready
+ * signal; Doppler role first WG: wait start, ready seen, freed signalled, tile done; range
+ * role last WG: after its ready signal).  Copies min(n_words, 4096) words of the last launch. */
+int fmcw_get_fused_trace(fmcw_handle* h, uint64_t* out, size_t n_words);
 int fmcw_kernel_times(fmcw_handle* h, double* ms, uint64_t* launches);
 int fmcw_reset_kernel_times(fmcw_handle* h);
 

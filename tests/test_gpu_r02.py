@@ -203,9 +203,16 @@ def test_compat_cfar_stage(kind):
     threshold wraps mod 2^17 and the 2-D bracket add wraps), fractions and out-of-range cells
     included; bit-exact vs cfar_os1d_rtl / cfar_os2d_rtl."""
     rng = np.random.default_rng(31)
-    m = rng.uniform(0, 140000, (2, 128, 128)).astype(np.float32)
-    m[0, ::7, ::5] = rng.uniform(25000, 60000, m[0, ::7, ::5].shape)
-    m[1, 20:40, 10:30] = rng.uniform(90000, 131000, (20, 20))
+    if kind == "os1d":
+        m = rng.uniform(0, 140000, (2, 128, 128)).astype(np.float32)
+        m[0, ::7, ::5] = rng.uniform(25000, 60000, m[0, ::7, ::5].shape)
+    else:
+        m = rng.uniform(5000, 15000, (2, 128, 128)).astype(np.float32)
+        m[0, 50, 60], m[1, 60, 100], m[1, 90, 3] = 131000.0, 120000.0, 70000.5
+        m[0, 10:12, :] = 150000.0                          # saturates at 2^17 - 1
+        m[0, 100, 5:9] = 2.0 ** 17 - 1.5
+    m[1, 20:40, 10:30] = rng.uniform(90000, 131000, (20, 20))   # mean ~1e5: the 17-bit bracket add wraps
+    m[1, 30, 20] = 131071.0
     m[1, 50, 50] = -5.0
     cf = O.Cfar1D() if kind == "os1d" else O.Cfar2D()
     with RadarCore(N_RANGE=128, N_DOPPLER=128, cfar=kind, compat_rtl=("cfar",), max_frames=2) as core:
@@ -360,3 +367,73 @@ def test_process_host_staging_is_reused():
     np.testing.assert_array_equal(a.rd_map[0], b.rd_map[0])
     np.testing.assert_array_equal(c.rd_map, b.rd_map[:2])
     np.testing.assert_array_equal(c.dets, b.dets[b.dets["frame"] < 2])
+
+
+@pytest.mark.parametrize("ns,nc,dtype,cfar,nf,extra", [
+    (1024, 256, "f32", "os1d", 13, {}),                       # BASELINE config 2, 13 frames (uneven over 8 XCDs)
+    (1024, 128, "i16", "os2d", 9, {}),                        # the reference core, 2-D CFAR after the fused map
+    (512, 256, "f16", "os1d", 3, {"magnitude": "ambm"}),
+    (2048, 128, "f32", "none", 2, {"map_kind": "db"}),
+    (1024, 256, "f32", "os1d", 1, {"cfar1d": (6, 1, 9, 3.0)}),
+])
+def test_fused_kernel_matches_k1_k2(monkeypatch, ns, nc, dtype, cfar, nf, extra):
+    """The fused range + Doppler kernel (one launch, spectrum in the XCD L2s) is bit-identical to
+    K1 -> HBM -> K2 (the same arithmetic in the same order), and on parity with the oracle."""
+    cube = synth.frames(nf, ns, nc, 1, "two_targets", dtype=dtype)
+    monkeypatch.setenv("FMCW_FUSED", "1")                     # opt-in path (fmcw.h FMCW_INFO_FUSED)
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, in_dtype=dtype, cfar=cfar, max_frames=nf, **extra) as core:
+        assert core.info("fused") == 1 and core.info("fused_group") >= 64
+        fused = core.process(cube)
+        assert core.info("fused_fallbacks") == 0
+    monkeypatch.setenv("FMCW_FUSED", "0")
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, in_dtype=dtype, cfar=cfar, max_frames=nf, **extra) as core:
+        assert core.info("fused") == 0
+        split = core.process(cube)
+    np.testing.assert_array_equal(fused.rd_map, split.rd_map)
+    np.testing.assert_array_equal(fused.dets, split.dets)
+    if extra.get("map_kind") != "db" and extra.get("magnitude") != "ambm":
+        ref = np.stack([O.process(to_complex(cube[f], dtype), None)["mag"] for f in range(nf)])
+        check_map(fused.rd_map, ref)
+        if cfar != "none":
+            cf = O.Cfar2D() if cfar == "os2d" else O.Cfar1D(*extra["cfar1d"]) if "cfar1d" in extra else O.Cfar1D()
+            np.testing.assert_array_equal(fused.dets, oracle_dets(fused.rd_map, cf))
+
+
+@pytest.mark.parametrize("env", [{"FMCW_FUSED": "1"}, {"FMCW_PIPE": "1", "FMCW_PIPE_CHUNK": "8"},
+                                 {"FMCW_PIPE": "1", "FMCW_PIPE_CHUNK": "5", "FMCW_PIPE_BUFS": "3"}])
+def test_repeated_launches_and_device_pointers(monkeypatch, env):
+    """Back-to-back launches on device buffers (the bench's pattern), fused kernel or the
+    two-stream K1/K2 chunk pipeline: every launch equals the first, batches of different sizes
+    included, and equals the serial K1 -> K2 path."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    ns, nc, F = 1024, 256, 64
+    uniq = synth.frames(8, ns, nc, 1, "random_target", seed=44)
+    cube = DeviceBuffer(F * uniq[0].nbytes)
+    for f in range(F):
+        cube.upload(uniq[f % 8], f * uniq[0].nbytes)
+    dmap = DeviceBuffer(F * ns * nc * 4)
+    cap = F * 4096
+    ddet = DeviceBuffer(cap * 16)
+    dn = DeviceBuffer(16)
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os1d", max_frames=F) as core:
+        assert core.info("fused") == (1 if "FMCW_FUSED" in env else 0)
+        runs = []
+        for nfr in (F, F, 17, F):
+            core.enqueue(cube, nfr, dmap, ddet, cap, dn)
+            n, dropped = (int(v) for v in dn.download(np.uint32, (2,)))
+            assert dropped == 0
+            runs.append((nfr, dmap.download(np.float32, (nfr, ns, nc)), ddet.download(DET_DTYPE, (n,))))
+    _, m0, d0 = runs[0]
+    for nfr, m, d in runs[1:]:
+        np.testing.assert_array_equal(m, m0[:nfr])
+        np.testing.assert_array_equal(d, d0[d0["frame"] < nfr])
+    for f in range(8, F):
+        np.testing.assert_array_equal(m0[f], m0[f % 8])
+    for k in env:
+        monkeypatch.delenv(k)
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os1d", max_frames=F) as core:
+        core.enqueue(cube, F, dmap, ddet, cap, dn)
+        n, _ = (int(v) for v in dn.download(np.uint32, (2,)))
+        np.testing.assert_array_equal(dmap.download(np.float32, (F, ns, nc)), m0)
+        np.testing.assert_array_equal(ddet.download(DET_DTYPE, (n,)), d0)

@@ -9,7 +9,7 @@ pids=()
 for spec in "$@"; do
   name=${spec%%=*}
   defs=${spec#*=}
-  /opt/rocm/bin/hipcc $FLAGS ${defs//,/ } -shared -o "lib/var_${name}.so" csrc/fmcw_api.hip csrc/tws_tracker.cpp &
+  /opt/rocm/bin/hipcc $FLAGS ${defs//,/ } -shared -o "lib/var_${name}.so" csrc/fmcw_api.hip csrc/fmcw_gather.hip csrc/tws_tracker.cpp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait "$p"; done
