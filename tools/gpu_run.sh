@@ -35,6 +35,8 @@ for s in "$@"; do
         FMCW_LIB="$PWD/$lib" run "ablib_${v#var_}" 300 python tools/ablate.py ${ABLATE_ARGS:-}
       done ;;
     counters) run counters 120 rocprofv3 -L ;;
+    prof_c*) w=${s#prof_}; run "rocprof_stats_$w" 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 5 --warmup 2 --no-cpu-baseline --no-h2d ;;
+    pmcsq_c*) w=${s#pmcsq_}; run "pmcsq_$w" 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/pmcsq_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
     pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_LDS_BANK_CONFLICT -d "$OUT/pmc_sq" -o run --output-format csv -- python3 tools/ablate.py --frames 256 --steps 2 --variants base ;;
     pmc_var_*) v=${s#pmc_var_}; run "pmc_$v" 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/pmc_$v" -o run --output-format csv -- python3 tools/ablate.py --frames 256 --steps 2 --variants "$v" ;;
     pmc2_var_*) v=${s#pmc2_var_}; run "pmc2_$v" 600 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_BUSY_CYCLES SQ_WAVES -d "$OUT/pmc2_$v" -o run --output-format csv -- python3 tools/ablate.py --frames 256 --steps 2 --variants "$v" ;;
