@@ -43,6 +43,19 @@ template <int NC> struct Cfar2DGeom {
   static constexpr int TPR = NC / 16;             // lanes per row
 };
 
+// The staged rows of one step: a ring of nr = TR + 2 hr rows of rs floats.  Tile row x (0 = the
+// first halo row of the current step) lives in slot (x + base) mod nr, so a strip of steps
+// keeps the 2 hr rows it shares with the next step and loads only TR new ones.
+struct RowRing {
+  float* tile;
+  int base, nr, rs;
+  __device__ __forceinline__ int slot(int x) const {
+    const int y = x + base;
+    return y >= nr ? y - nr : y;
+  }
+  __device__ __forceinline__ float* row(int x) const { return tile + slot(x) * rs; }
+};
+
 __device__ __forceinline__ uint32_t f2key(float f) {
   const uint32_t u = __float_as_uint(f);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -51,15 +64,18 @@ __device__ __forceinline__ float key2f(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
-#ifndef FMCW_CFAR2D_SCREEN  // phase A as pair screen + exact count of the survivors (1) or exact (0)
-#define FMCW_CFAR2D_SCREEN 1
+#ifndef FMCW_CFAR2D_SCREEN  // phase A: packed 16-bit pair screen (2), fp32 pair screen (1), exact (0);
+#define FMCW_CFAR2D_SCREEN 2  // the screens are followed by the exact count of their survivors
 #endif
-constexpr int kCfar2dList = 128;  // u32 per wave after the rows: 64 survivor cells + 64 verdicts
+#ifndef FMCW_CFAR2D_PREFETCH  // load a strip's next rows during the current step (1)
+#define FMCW_CFAR2D_PREFETCH 1
+#endif
+constexpr int kCfar2dList = 2 * 256 + 16;  // u32 after the rows: round list, verdicts / positions, counts
 
 template <int NC>
 constexpr size_t cfar2d_smem_bytes(int hr) {
   using G = Cfar2DGeom<NC>;
-  return (size_t)(G::TR + 2 * hr) * G::RS * 4 + (FMCW_CFAR2D_SCREEN ? G::WPB * kCfar2dList * 4 : 0);
+  return (size_t)(G::TR + 2 * hr) * G::RS * 4 + kCfar2dList * 4;
 }
 
 // Phase A screen (compile-time HD / GD): disjoint PAIRS of Doppler-adjacent references.  A pair
@@ -70,15 +86,14 @@ constexpr size_t cfar2d_smem_bytes(int hr) {
 // On noise + targets about 5 % of the cells pass (0.6 % pass the exact count) at half the
 // compares; the survivors are then counted exactly, one per lane.
 template <int NC, int HD, int GD>
-__device__ __forceinline__ uint32_t cfar2d_screen(const float* tile, int rl, int d0, const Cfar2DArgs& a,
+__device__ __forceinline__ uint32_t cfar2d_screen(const RowRing& rr, int rl, int d0, const Cfar2DArgs& a,
                                                   int need) {
-  constexpr int RS = Cfar2DGeom<NC>::RS;
   static_assert(HD <= MH, "the window stays inside the row halos");
   constexpr int W = 16 + 2 * HD;
   constexpr int O0 = floor4(-HD);
   constexpr int NV = (W + (-HD - O0) + 3) / 4;
   constexpr int SEG = HD - GD, NPS = SEG / 2;   // guard-row segment length, pairs per segment
-  const float* lb = tile + (rl + a.hr) * RS + midx(d0);
+  const float* lb = rr.row(rl + a.hr) + midx(d0);
   uint32_t cb[16], nlt[16];  // cut bits; #{pairs with fl(s_min * min) < cut}
   {
     float c[16];
@@ -91,7 +106,7 @@ __device__ __forceinline__ uint32_t cfar2d_screen(const float* tile, int rl, int
   }
   for (int dr = -a.hr; dr <= a.hr; ++dr) {
     float v[4 * NV];
-    load_cells<NV>(lb + dr * RS, O0, v);
+    load_cells<NV>(rr.row(rl + a.hr + dr) + midx(d0), O0, v);
     uint32_t pm[W - 1];  // pm[k] = fl(s_min * min(cell k, cell k + 1)), cell 0 = d0 - HD
 #pragma unroll
     for (int k = 0; k < W - 1; ++k)
@@ -117,41 +132,134 @@ __device__ __forceinline__ uint32_t cfar2d_screen(const float* tile, int rl, int
   return bits;
 }
 
-// Exact phase-A test of one cell (CUT row rl of the group tile, Doppler d): candidate <=>
-// #{fl(s_min * ref) >= cut} < need.  Addresses: midx(d + dd) with a runtime d.
+// The same pair screen on packed 16-bit keys, two CUTs per VALU op.  The key of a cell is the
+// high half of its bit pattern (cells are non-negative: sign 0, 8 exponent and 7 mantissa
+// bits), monotone in the value, so min() commutes with it.  Each CUT gets the key of
+// q = fl(cut / s_min) + 8 ulps (cut * fl(1 / s_min): <= 2 ulps of error), and a pair counts
+// only if its min key is STRICTLY above that key: then min > q > cut / s_min in reals, so both
+// refs have s_min * ref > cut and fl(s_min * ref) >= cut -- still a lower bound on the exact
+// count (the key's 2^-7 resolution only makes the screen a little weaker).  Per window row:
+// 27 byte-perms build hi16 pairs, 26 v_pk_min_u16 the packed pair minima, and each
+// (two CUTs, one pair) step is v_pk_sub_u16 + v_pk_lshrrev_b16 + v_pk_add_u16 (bit 15 of
+// pairmin - (key + 1) is set iff pairmin <= key).  No multiplies in the row loop.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
 template <int NC, int HD, int GD>
-__device__ __forceinline__ bool cfar2d_exact_a(const float* tile, int rl, int d, const Cfar2DArgs& a, int need) {
-  constexpr int RS = Cfar2DGeom<NC>::RS;
-  const float* crow = tile + (rl + a.hr) * RS;
+__device__ __forceinline__ uint32_t cfar2d_screen16(const RowRing& rr, int rl, int d0, const Cfar2DArgs& a,
+                                                    int need) {
+  static_assert(HD <= MH, "the window stays inside the row halos");
+  constexpr int W = 16 + 2 * HD;
+  constexpr int O0 = floor4(-HD);
+  constexpr int NV = (W + (-HD - O0) + 3) / 4;
+  constexpr int SEG = HD - GD, NPS = SEG / 2;
+  const float* lb = rr.row(rl + a.hr) + midx(d0);
+  const float inv_s = 1.0f / a.s_min;
+  u16x2 ck[8], nlt[8];  // (key + 1) of CUTs 2p, 2p + 1; #{pairs not counted}
+  {
+    float c[16];
+    load_cells<4>(lb, 0, c);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const uint32_t k0 = min((__float_as_uint(c[2 * p] * inv_s) + 8u) >> 16, 0x7fffu) + 1u;
+      const uint32_t k1 = min((__float_as_uint(c[2 * p + 1] * inv_s) + 8u) >> 16, 0x7fffu) + 1u;
+      ck[p] = __builtin_bit_cast(u16x2, k0 | (k1 << 16));
+      nlt[p] = (u16x2)(0);
+    }
+  }
+  for (int dr = -a.hr; dr <= a.hr; ++dr) {
+    float v[4 * NV];
+    load_cells<NV>(rr.row(rl + a.hr + dr) + midx(d0), O0, v);
+    u16x2 P[W - 2];  // P[k] = (pairmin key k, pairmin key k + 1), cell 0 = d0 - HD
+    {
+      uint32_t V[W - 1];  // V[k] = (key of cell k, key of cell k + 1)
+#pragma unroll
+      for (int k = 0; k < W - 1; ++k)
+        V[k] = __builtin_amdgcn_perm(__float_as_uint(v[-HD - O0 + k + 1]), __float_as_uint(v[-HD - O0 + k]),
+                                     0x07060302u);
+#pragma unroll
+      for (int k = 0; k < W - 2; ++k)
+        P[k] = __builtin_elementwise_min(__builtin_bit_cast(u16x2, V[k]), __builtin_bit_cast(u16x2, V[k + 1]));
+    }
+    if (dr >= -a.gr && dr <= a.gr) {  // guard row (uniform branch)
+#pragma unroll
+      for (int p = 0; p < 8; ++p)
+#pragma unroll
+        for (int j = 0; j < NPS; ++j) {
+          nlt[p] += (u16x2)(P[2 * p + 2 * j] - ck[p]) >> (unsigned short)15;
+          nlt[p] += (u16x2)(P[2 * p + HD + GD + 1 + 2 * j] - ck[p]) >> (unsigned short)15;
+        }
+    } else {
+#pragma unroll
+      for (int p = 0; p < 8; ++p)
+#pragma unroll
+        for (int j = 0; j < HD; ++j) nlt[p] += (u16x2)(P[2 * p + 2 * j] - ck[p]) >> (unsigned short)15;
+    }
+  }
+  const int n_guard = 2 * a.gr + 1;
+  const int np = (2 * a.hr + 1 - n_guard) * HD + n_guard * 2 * NPS;  // pairs per cell
+  uint32_t bits = 0;
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    bits |= (2 * (np - (int)nlt[p].x) < need ? 1u : 0u) << (2 * p);
+    bits |= (2 * (np - (int)nlt[p].y) < need ? 1u : 0u) << (2 * p + 1);
+  }
+  return bits;
+}
+
+// Exact candidate test of one cell (CUT row rl of the group tile, Doppler d), one lane per
+// cell.  With E(s) = #{fl(s * ref) >= cut}, the cell can only detect if E(s) < need for the
+// scale s it gets.  E(s_min) >= need rules every scale out.  The scale is sc_min only when
+// #{ref < mean / 2} >= rank + 1 (os_cfar_2d.vhd:195-199); otherwise it is >= s2 =
+// min(sc_nom, sc_max) and E(s2) >= need rules the cell out too.  #{ref < mean / 2} is bounded
+// from above with any-order fp32 sum x (1 + 2^-15) (the sum of <= 128 non-negative terms in
+// another order differs by < 2^-16 relative; compat's integer sums are exact), so the test
+// keeps every cell that can detect.  On single-channel (Rayleigh) maps it drops ~99 % of the
+// cells E(s_min) alone passes.  Addresses: midx(d + dd) with a runtime d.
+template <int NC, int HD, int GD>
+__device__ __forceinline__ bool cfar2d_exact_a(const RowRing& rr, int rl, int d, const Cfar2DArgs& a, int need) {
+  const float* crow = rr.row(rl + a.hr);
   const int x = d + MH;
   auto at = [&](const float* row, int dd) { return row[(x + dd) + (((x + dd) >> 4) << 2)]; };
   const uint32_t cbits = __float_as_uint(at(crow, 0));
-  uint32_t lt = 0;
-  for (int dr = -a.hr; dr <= a.hr; ++dr) {
-    const float* row = crow + dr * RS;
-    if (dr >= -a.gr && dr <= a.gr) {
+  const float s2 = a.override_ ? a.s_min : fminf(a.sc_nom, a.sc_max);
+  uint32_t lt = 0, lt2 = 0;
+  float sum = 0.f;
+  auto visit = [&](auto&& fn) {
+    for (int dr = -a.hr; dr <= a.hr; ++dr) {
+      const float* row = rr.row(rl + a.hr + dr);
+      if (dr >= -a.gr && dr <= a.gr) {
 #pragma unroll
-      for (int dd = -HD; dd <= HD; ++dd)
-        if (dd < -GD || dd > GD) lt += lt_bit(__float_as_uint(a.s_min * at(row, dd)), cbits);
-    } else {
+        for (int dd = -HD; dd <= HD; ++dd)
+          if (dd < -GD || dd > GD) fn(at(row, dd));
+      } else {
 #pragma unroll
-      for (int dd = -HD; dd <= HD; ++dd) lt += lt_bit(__float_as_uint(a.s_min * at(row, dd)), cbits);
+        for (int dd = -HD; dd <= HD; ++dd) fn(at(row, dd));
+      }
     }
-  }
-  return (int)lt > a.n_ref - need;
+  };
+  visit([&](float v) {
+    lt += lt_bit(__float_as_uint(a.s_min * v), cbits);
+    lt2 += lt_bit(__float_as_uint(s2 * v), cbits);
+    sum += v;
+  });
+  if ((int)lt <= a.n_ref - need) return false;                // E(s_min) >= need
+  if ((int)lt2 > a.n_ref - need || a.override_) return true;  // E(s2) < need
+  const float half_up = sum * (1.0f + 1.0f / 32768.0f) / (float)a.n_ref * 0.5f;
+  uint32_t n_lo = 0;
+  visit([&](float v) { n_lo += v < half_up ? 1u : 0u; });
+  return (int)n_lo >= a.rank + 1;                             // sc_min still possible
 }
 
 // Phase A for a compile-time Doppler extent HD / guard GD; returns this lane's candidate bits.
 // `rl` is the CUT row within the workgroup tile (tile row rl + hr).
 template <int NC, int HD, int GD>
-__device__ __forceinline__ uint32_t cfar2d_phase_a(const float* tile, int rl, int d0, const Cfar2DArgs& a,
+__device__ __forceinline__ uint32_t cfar2d_phase_a(const RowRing& rr, int rl, int d0, const Cfar2DArgs& a,
                                                    int need) {
-  constexpr int RS = Cfar2DGeom<NC>::RS;
   static_assert(HD <= MH, "the window stays inside the row halos");
   constexpr int W = 16 + 2 * HD;
   constexpr int O0 = floor4(-HD);
   constexpr int NV = (W + (-HD - O0) + 3) / 4;
-  const float* lb = tile + (rl + a.hr) * RS + midx(d0);
+  const float* lb = rr.row(rl + a.hr) + midx(d0);
   uint32_t cb[16], lt[16];   // cut bits; #{fl(s_min * ref) < cut} (lt_bit: no SGPR masks)
   {
     float c[16];
@@ -164,7 +272,7 @@ __device__ __forceinline__ uint32_t cfar2d_phase_a(const float* tile, int rl, in
   }
   for (int dr = -a.hr; dr <= a.hr; ++dr) {
     float v[4 * NV];
-    load_cells<NV>(lb + dr * RS, O0, v);
+    load_cells<NV>(rr.row(rl + a.hr + dr) + midx(d0), O0, v);
     uint32_t sb[W];
 #pragma unroll
     for (int k = 0; k < W; ++k) sb[k] = __float_as_uint(a.s_min * v[-HD - O0 + k]);
@@ -190,17 +298,16 @@ __device__ __forceinline__ uint32_t cfar2d_phase_a(const float* tile, int rl, in
 
 // Phase A, runtime geometry (any window the LDS budget allows; Doppler wraps explicitly).
 template <int NC>
-__device__ __forceinline__ uint32_t cfar2d_phase_a_generic(const float* tile, int rl, int d0,
+__device__ __forceinline__ uint32_t cfar2d_phase_a_generic(const RowRing& rr, int rl, int d0,
                                                            const Cfar2DArgs& a, int need) {
-  constexpr int RS = Cfar2DGeom<NC>::RS;
-  const float* crow = tile + (rl + a.hr) * RS;
+  const float* crow = rr.row(rl + a.hr);
   uint32_t bits = 0;
   for (int i = 0; i < 16; ++i) {
     const int d = d0 + i;
     const uint32_t c = __float_as_uint(crow[midx(d)]);
     uint32_t lt = 0;
     for (int dr = -a.hr; dr <= a.hr; ++dr) {
-      const float* row = crow + dr * RS;
+      const float* row = rr.row(rl + a.hr + dr);
       const bool grow = dr >= -a.gr && dr <= a.gr;
       for (int dd = -a.hd; dd <= a.hd; ++dd) {
         if (grow && dd >= -a.gd && dd <= a.gd) continue;
@@ -232,12 +339,80 @@ __device__ __forceinline__ void cfar2d_ref_offset(const Cfar2DArgs& a, int j, in
   }
 }
 
+// ---- Workgroup-cooperative rounds over a set of cells.  Each lane owns up to 16 cells (bits of
+// `m`); the workgroup's cells, in (wave, lane, bit) order == tile order, are listed 256 per round
+// in `list` as (wave << 10 | lane << 4 | bit) and handed to fn(n) between two barriers.  With
+// `pos` the entry's running position pos0 + (its index among the lane's bits) goes alongside.
+// Every wave of the workgroup must call this (barriers); `cnt` holds 4 words of its own.
+constexpr int kCoopRound = 256;
+template <class Fn>
+__device__ __forceinline__ void coop_rounds(uint32_t m, uint32_t* cnt, uint32_t* list, uint32_t* pos,
+                                            uint32_t pos0, Fn&& fn) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int n_w;
+  const int ex = wave_excl_scan(__popc(m), n_w);
+  if (lane == 0) cnt[wv] = (uint32_t)n_w;
+  __syncthreads();
+  int off = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = (int)cnt[i];
+    off += i < wv ? c : 0;
+    tot += c;
+  }
+  for (int b0 = 0; b0 < tot; b0 += kCoopRound) {  // uniform over the workgroup
+    int o = off + ex, t = 0;
+    for (uint32_t mm = m; mm; mm &= mm - 1, ++o, ++t)
+      if (o >= b0 && o < b0 + kCoopRound) {
+        list[o - b0] = ((uint32_t)wv << 10) | ((uint32_t)lane << 4) | (uint32_t)__builtin_ctz(mm);
+        if (pos) pos[o - b0] = pos0 + (uint32_t)t;
+      }
+    __syncthreads();
+    fn(min(kCoopRound, tot - b0));
+    __syncthreads();  // the next round rewrites the list
+  }
+}
+
+// k-th smallest (0-based) of the wave's keys ka (lanes in ma) and kb (lanes in mb), by
+// pivoting: the pivot is the median of three active keys, ballots count the keys below and
+// equal to it, and the active set shrinks to the side holding rank k.  Every step removes at
+// least the pivot's equals, so it ends; on these windows it takes ~6-10 steps where a bitwise
+// radix select takes 32.  Wave-uniform control flow; needs k < #active.
+__device__ __forceinline__ uint32_t wave_select_kth(uint32_t ka, uint32_t kb, uint64_t ma, uint64_t mb, int k) {
+  for (int it = 0; it < 256; ++it) {  // bound: >= 1 key leaves per step, 128 keys
+    const uint64_t m1 = ma ? ma : mb;
+    const uint32_t v1 = ma ? ka : kb;
+    const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)v1, __builtin_ctzll(m1));
+    const uint32_t p2 = (uint32_t)__builtin_amdgcn_readlane((int)v1, 63 - __builtin_clzll(m1));
+    const uint64_t m3 = mb ? mb : ma;
+    const uint32_t v3 = mb ? kb : ka;
+    const uint64_t m3r = m3 & (m3 - 1);  // second active lane when there is one
+    const uint32_t p3 = (uint32_t)__builtin_amdgcn_readlane((int)v3, __builtin_ctzll(m3r ? m3r : m3));
+    const uint32_t p = max(min(p1, p2), min(max(p1, p2), p3));
+    const uint64_t la = __ballot(ka < p) & ma, ea = __ballot(ka == p) & ma;
+    const uint64_t lb = __ballot(kb < p) & mb, eb = __ballot(kb == p) & mb;
+    const int lt = __popcll(la) + __popcll(lb), eq = __popcll(ea) + __popcll(eb);
+    if (k < lt) {
+      ma = la;
+      mb = lb;
+    } else if (k < lt + eq) {
+      return p;
+    } else {
+      k -= lt + eq;
+      ma &= ~(la | ea);
+      mb &= ~(lb | eb);
+    }
+  }
+  return 0u;  // unreachable for k < #active
+}
+
 template <int NC, int HD, int GD>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
-k_cfar2d(const float* __restrict__ map, int ns, int n_wg_tiles, int frame0, int tile0, Cfar2DArgs a,
+k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int frame0, int tile0, Cfar2DArgs a,
          DetSink sink) {
   using Gm = Cfar2DGeom<NC>;
-  constexpr int WR = Gm::WR, NT = Gm::NT, RS = Gm::RS, TPR = Gm::TPR, WPB = Gm::WPB;
+  constexpr int WR = Gm::WR, NT = Gm::NT, RS = Gm::RS, TPR = Gm::TPR, WPB = Gm::WPB, TR = Gm::TR;
+  static_assert(TR * NC == 4 * 4 * NT, "a step's new rows are 4 float4 per thread");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* const tile = smem;
 
@@ -248,192 +423,207 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_wg_tiles, int frame0, int 
   cfar2d_ref_offset(a, lane, dra, dda);
   cfar2d_ref_offset(a, lane + 64, drb, ddb);
   const bool oka = lane < a.n_ref, okb = lane + 64 < a.n_ref;
-  const int offa = dra * RS, offb = drb * RS;
   const int need = a.n_ref - a.rank;
   const int wt_per_frame = ns / WR;                      // wave tiles per frame
   const int wg_per_frame = (wt_per_frame + WPB - 1) / WPB;
-  const int nf = n_wg_tiles / wg_per_frame;
+  const int spf = (wg_per_frame + steps - 1) / steps;    // strips per frame
+  const int nf = n_strips / spf;
+  const int nr = TR + 2 * a.hr;                          // ring rows
+  uint32_t* const list = reinterpret_cast<uint32_t*>(tile + nr * RS);
+  uint32_t* const aux = list + kCoopRound;
+  uint32_t* const cnt = aux + kCoopRound;
+  const int tid = opaque(threadIdx.x);
 
-  for (int g = blockIdx.x; g < n_wg_tiles; g += gridDim.x) {
-    // frame-minor order (as K2): hot rows (targets) spread over all workgroups
+  // one float4 of cells (row x, Doppler d..d+3) into the ring, with its circular-halo copy
+  auto put4 = [&](const RowRing& rr, int x, int d, float4 v) {
+    v = a.compat ? q17x4(v) : nonneg4(v);
+    float* row = rr.row(x);
+    *reinterpret_cast<float4*>(row + midx(d)) = v;
+    if (d < MH) *reinterpret_cast<float4*>(row + midx(NC + d)) = v;
+    if (d >= NC - MH) *reinterpret_cast<float4*>(row + midx(d - NC)) = v;
+  };
+
+  for (int g = blockIdx.x; g < n_strips; g += gridDim.x) {
+    // a strip: `steps` consecutive workgroup tiles of one frame (frame-minor order, as K2:
+    // hot rows spread over all workgroups); each step tests TR rows and loads only TR new ones
     const int f = g % nf;
-    const int wt0 = (g / nf) * WPB;                      // first wave tile of this group
-    const int n_wt = min(WPB, wt_per_frame - wt0);
-    const int r0 = wt0 * WR;                             // first CUT row of this group
-    const int rows_in = n_wt * WR + 2 * a.hr;
-    const int tid = opaque(threadIdx.x);
-    __syncthreads();  // the previous group's waves are done with the rows
-    {
-      // rows r0-hr .. r0+n_wt*WR+hr-1 (zero outside the map), 4 float4 loads in flight per lane
-      const float* fm = map + (size_t)f * ns * NC;
-      const int n4 = rows_in * (NC / 4);
-      for (int b = tid; b < n4; b += 4 * NT) {
-        float4 v[4];
+    const int t_beg = (g / nf) * steps, t_end = min(t_beg + steps, wg_per_frame);
+    const float* fm = map + (size_t)f * ns * NC;
+    RowRing rr{tile, 0, nr, RS};
+    float4 pre[4];
+    for (int t = t_beg; t < t_end; ++t) {
+      const int wt0 = t * WPB;                             // first wave tile of this step
+      const int n_wt = min(WPB, wt_per_frame - wt0);
+      const int r0 = wt0 * WR;                             // first CUT row of this step
+      __syncthreads();  // the previous step's waves are done with the rows and the lists
+      if (t == t_beg) {
+        // rows r0-hr .. r0+TR+hr-1 (zero outside the map), 4 float4 loads in flight per lane
+        const int n4 = nr * (NC / 4);
+        for (int b = tid; b < n4; b += 4 * NT) {
+          float4 v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int e4 = b + u * NT;
-          const int rl = e4 / (NC / 4), d = (e4 - rl * (NC / 4)) * 4;
-          const int r = r0 - a.hr + rl;
-          v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (e4 < n4 && r >= 0 && r < ns) v[u] = *reinterpret_cast<const float4*>(fm + (size_t)r * NC + d);
-        }
+          for (int u = 0; u < 4; ++u) {
+            const int e4 = b + u * NT;
+            const int x = e4 / (NC / 4), d = (e4 - x * (NC / 4)) * 4;
+            const int r = r0 - a.hr + x;
+            v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (e4 < n4 && r >= 0 && r < ns) v[u] = *reinterpret_cast<const float4*>(fm + (size_t)r * NC + d);
+          }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int e4 = b + u * NT;
-          if (e4 < n4) {
-            const int rl = e4 / (NC / 4), d = (e4 - rl * (NC / 4)) * 4;
-            *reinterpret_cast<float4*>(tile + rl * RS + midx(d)) = a.compat ? q17x4(v[u]) : nonneg4(v[u]);
+          for (int u = 0; u < 4; ++u) {
+            const int e4 = b + u * NT;
+            const int x = e4 / (NC / 4), d = (e4 - x * (NC / 4)) * 4;
+            if (e4 < n4) put4(rr, x, d, v[u]);
           }
         }
-      }
-    }
-    __syncthreads();
-    for (int e = tid; e < rows_in * 2 * MH; e += NT) {   // circular Doppler halos
-      const int rl = e / (2 * MH), j = e - rl * (2 * MH);
-      const int dst = j < MH ? NC + j : j - 2 * MH;
-      const int src = j < MH ? j : NC + j - 2 * MH;
-      tile[rl * RS + midx(dst)] = tile[rl * RS + midx(src)];
-    }
-    __syncthreads();
-    if (wv >= n_wt) continue;  // uniform per wave: no wave tile left in this frame
-
-    // ---- Phase A: candidates among this lane's 16 cells
-    const int rlw = wv * WR + lane / TPR;    // CUT row within the group tile
-    const int d0 = (lane % TPR) * 16;
-    const int r = r0 + rlw;
-    uint32_t cand = 0;
-    if (r >= a.hr && r < ns - a.hr) {
-      if constexpr (HD > 0) {
-        if constexpr (FMCW_CFAR2D_SCREEN) cand = cfar2d_screen<NC, HD, GD>(tile, rlw, d0, a, need);
-        else cand = cfar2d_phase_a<NC, HD, GD>(tile, rlw, d0, a, need);
       } else {
-        cand = cfar2d_phase_a_generic<NC>(tile, rlw, d0, a, need);
-      }
-    }
-    if constexpr (HD > 0 && FMCW_CFAR2D_SCREEN) {
-      // survivors of the screen -> exact test, 64 per round, one per lane, in cell order
-      uint32_t* const lst = reinterpret_cast<uint32_t*>(tile + (Gm::TR + 2 * a.hr) * RS) + wv * kCfar2dList;
-      uint32_t* const ver = lst + 64;
-      const uint32_t scr = cand;
-      cand = 0;
-      int n_s;
-      const int sx = wave_excl_scan(__popc(scr), n_s);
-      for (int base_s = 0; base_s < n_s; base_s += 64) {  // uniform
-        {
-          int o = sx;
-          for (uint32_t m = scr; m; m &= m - 1, ++o)
-            if (o >= base_s && o < base_s + 64) lst[o - base_s] = ((uint32_t)lane << 4) | (uint32_t)__builtin_ctz(m);
-        }
-        pass_sync<false>();
-        if (base_s + lane < n_s) {
-          const uint32_t e = lst[lane];
-          const int src = (int)(e >> 4), i = (int)(e & 15u);
-          ver[lane] = cfar2d_exact_a<NC, HD, GD>(tile, wv * WR + src / TPR, (src % TPR) * 16 + i, a, need) ? 1u : 0u;
-        }
-        pass_sync<false>();
-        {
-          int o = sx;
-          for (uint32_t m = scr; m; m &= m - 1, ++o)
-            if (o >= base_s && o < base_s + 64 && ver[o - base_s]) cand |= 1u << __builtin_ctz(m);
-        }
-        pass_sync<false>();  // the next round rewrites lst / ver
-      }
-    }
-
-    // ---- Phase B helpers: the wave's view of candidate cell (row l0 / TPR of the wave, d)
-    auto refs_of = [&](int l0, int d, float& va, float& vb) {
-      const float* crow = tile + (wv * WR + l0 / TPR + a.hr) * RS;
-      va = oka ? crow[offa + midx((d + dda) & (NC - 1))] : 0.f;
-      vb = okb ? crow[offb + midx((d + ddb) & (NC - 1))] : 0.f;
-    };
-    auto scale_of = [&](float va, float vb) -> float {
-      float sum = va + vb;
+        // the ring turns by TR rows; the TR new rows (prefetched during the previous step) go
+        // into the slots of the TR rows that left
+        rr.base += TR;
+        if (rr.base >= nr) rr.base -= nr;
 #pragma unroll
-      for (int x = 32; x >= 1; x >>= 1) sum += __shfl_xor(sum, x, 64);
-      if (a.override_) return (float)a.override_;
-      float half, hi;
-      if (a.compat) {
-        // integer cells < 2^17, <= 128 of them: every partial sum < 2^24 is exact in fp32.
-        // mean = floor(sum / N_REF) (os_cfar_2d.vhd:189); the bracket add is 17 bits wide (:193)
-        const uint32_t mean = (uint32_t)sum / (uint32_t)a.n_ref;
-        half = (float)(mean >> 1);
-        hi = (float)((mean + (mean >> 1)) & kQ17Mask);
-      } else {
-        const float mean = sum / (float)a.n_ref;
-        half = mean * 0.5f;
-        hi = mean + half;
+        for (int u = 0; u < 4; ++u) {
+          const int e4 = tid + u * NT;
+          const int i = e4 / (NC / 4), d = (e4 - i * (NC / 4)) * 4;
+          if (!FMCW_CFAR2D_PREFETCH) {
+            const int rn = r0 + a.hr + i;  // new row of this step (zero past the map)
+            pre[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (rn < ns) pre[u] = *reinterpret_cast<const float4*>(fm + (size_t)rn * NC + d);
+          }
+          put4(rr, nr - TR + i, d, pre[u]);
+        }
       }
-      const int n_hi = __popcll(__ballot(oka && va > hi)) + __popcll(__ballot(okb && vb > hi));
-      const int n_lo = __popcll(__ballot(oka && va < half)) + __popcll(__ballot(okb && vb < half));
-      return (n_hi >= need) ? a.sc_max : (n_lo >= a.rank + 1) ? a.sc_min : a.sc_nom;
-    };
+      if (FMCW_CFAR2D_PREFETCH && t + 1 < t_end) {  // prefetch the next step's new rows r0 + TR + hr ..
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e4 = tid + u * NT;
+          const int i = e4 / (NC / 4), d = (e4 - i * (NC / 4)) * 4;
+          const int r = r0 + TR + a.hr + i;
+          pre[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (r < ns) pre[u] = *reinterpret_cast<const float4*>(fm + (size_t)r * NC + d);
+        }
+      }
+      __syncthreads();
+      const bool has_tile = wv < n_wt;  // uniform per wave; waves without a tile still join the barriers
 
-    // ---- Phase B pass 1: decide every candidate (cell order); detections -> owner's bits
-    uint32_t detw = 0;
-    {
-      uint64_t nz = __ballot(cand != 0);
-      while (nz) {
-        const int l0 = __builtin_ctzll(nz);
-        nz &= nz - 1;
-        uint32_t bits = (uint32_t)__shfl((int)cand, l0, 64);
-        while (bits) {
-          const int i = __builtin_ctz(bits);
-          bits &= bits - 1;
-          const int d = (l0 % TPR) * 16 + i;
-          const float cut = tile[(wv * WR + l0 / TPR + a.hr) * RS + midx(d)];
+      // ---- Phase A: candidates among this lane's 16 cells
+      const int rlw = wv * WR + lane / TPR;    // CUT row within the group tile
+      const int d0 = (lane % TPR) * 16;
+      const int r = r0 + rlw;
+      uint32_t cand = 0;
+      if (has_tile && r >= a.hr && r < ns - a.hr) {
+        if constexpr (HD > 0) {
+          if constexpr (FMCW_CFAR2D_SCREEN == 2) cand = cfar2d_screen16<NC, HD, GD>(rr, rlw, d0, a, need);
+          else if constexpr (FMCW_CFAR2D_SCREEN) cand = cfar2d_screen<NC, HD, GD>(rr, rlw, d0, a, need);
+          else cand = cfar2d_phase_a<NC, HD, GD>(rr, rlw, d0, a, need);
+        } else {
+          cand = cfar2d_phase_a_generic<NC>(rr, rlw, d0, a, need);
+        }
+      }
+      // cell of a round-list entry (wave << 10 | lane << 4 | bit) -> group-tile row, Doppler bin
+      auto cell_of = [&](uint32_t e, int& trow, int& d) {
+        const int we = (int)(e >> 10), le = (int)((e >> 4) & 63u);
+        trow = we * WR + le / TPR;
+        d = (le % TPR) * 16 + (int)(e & 15u);
+      };
+      if constexpr (HD > 0 && FMCW_CFAR2D_SCREEN) {
+        // survivors of the screen -> exact count, one lane per cell, 256 per round over the
+        // whole workgroup (a hot tile's survivors spread over all four waves)
+        aux[threadIdx.x] = 0u;
+        const uint32_t scr = cand;
+        coop_rounds(scr, cnt, list, nullptr, 0u, [&](int n) {
+          if ((int)threadIdx.x < n) {
+            int trow, d;
+            const uint32_t e = list[threadIdx.x];
+            cell_of(e, trow, d);
+            if (cfar2d_exact_a<NC, HD, GD>(rr, trow, d, a, need))
+              atomicOr(&aux[e >> 4], 1u << (e & 15u));
+          }
+        });
+        cand = aux[threadIdx.x];
+        __syncthreads();  // every lane has its bits before aux is cleared again
+      }
+
+      // ---- Phase B: one whole wave per candidate cell.  Lanes hold refs l and l + 64 of the fixed
+      // order; the mean is the fixed fp32 halving tree; the scale bracket comes from ballot counts.
+      auto refs_of = [&](int trow, int d, float& va, float& vb) {
+        va = oka ? rr.row(trow + a.hr + dra)[midx((d + dda) & (NC - 1))] : 0.f;
+        vb = okb ? rr.row(trow + a.hr + drb)[midx((d + ddb) & (NC - 1))] : 0.f;
+      };
+      auto scale_of = [&](float va, float vb) -> float {
+        float sum = va + vb;
+#pragma unroll
+        for (int x = 32; x >= 1; x >>= 1) sum += __shfl_xor(sum, x, 64);
+        if (a.override_) return (float)a.override_;
+        float half, hi;
+        if (a.compat) {
+          // integer cells < 2^17, <= 128 of them: every partial sum < 2^24 is exact in fp32.
+          // mean = floor(sum / N_REF) (os_cfar_2d.vhd:189); the bracket add is 17 bits wide (:193)
+          const uint32_t mean = (uint32_t)sum / (uint32_t)a.n_ref;
+          half = (float)(mean >> 1);
+          hi = (float)((mean + (mean >> 1)) & kQ17Mask);
+        } else {
+          const float mean = sum / (float)a.n_ref;
+          half = mean * 0.5f;
+          hi = mean + half;
+        }
+        const int n_hi = __popcll(__ballot(oka && va > hi)) + __popcll(__ballot(okb && vb > hi));
+        const int n_lo = __popcll(__ballot(oka && va < half)) + __popcll(__ballot(okb && vb < half));
+        return (n_hi >= need) ? a.sc_max : (n_lo >= a.rank + 1) ? a.sc_min : a.sc_nom;
+      };
+#ifdef FMCW_CFAR2D_ABLATE  // timing experiments only: 1 = no phase B, 2 = no ranked-value select
+      if (FMCW_CFAR2D_ABLATE == 1) cand = 0;
+#endif
+
+      // Pass 1: decide every candidate; the four waves take the round's entries in turn
+      aux[threadIdx.x] = 0u;
+      coop_rounds(cand, cnt + 4, list, nullptr, 0u, [&](int n) {
+        for (int j = wv; j < n; j += WPB) {
+          int trow, d;
+          const uint32_t e = list[j];
+          cell_of(e, trow, d);
+          const float cut = rr.row(trow + a.hr)[midx(d)];
           float va, vb;
-          refs_of(l0, d, va, vb);
+          refs_of(trow, d, va, vb);
           const float sc = scale_of(va, vb);
           const int n_ge = __popcll(__ballot(oka && sc * va >= cut)) + __popcll(__ballot(okb && sc * vb >= cut));
-          if (n_ge < need && lane == l0) detw |= 1u << i;
+          if (n_ge < need && lane == 0) atomicOr(&aux[e >> 4], 1u << (e & 15u));
         }
-      }
-    }
-    int total;
-    (void)wave_excl_scan(__popc(detw), total);
-    const int wtile = tile0 + f * wt_per_frame + wt0 + wv;
-    const uint32_t base = det_reserve_wave(sink, wtile, total);
+      });
+      const uint32_t detw = aux[threadIdx.x];
+      int total;
+      const int dx = wave_excl_scan(__popc(detw), total);
+      const int wtile = tile0 + f * wt_per_frame + wt0 + wv;
+      const uint32_t base = has_tile ? det_reserve_wave(sink, wtile, total) : 0u;
+      __syncthreads();  // aux now carries sink positions
 
-    // ---- Phase B pass 2: exact ranked value (k-th smallest) of each detection, in order
-    uint32_t o = 0;
-    uint64_t nz = __ballot(detw != 0);
-    while (nz) {
-      const int l0 = __builtin_ctzll(nz);
-      nz &= nz - 1;
-      uint32_t bits = (uint32_t)__shfl((int)detw, l0, 64);
-      while (bits) {
-        const int i = __builtin_ctz(bits);
-        bits &= bits - 1;
-        const int d = (l0 % TPR) * 16 + i;
-        const int rl = wv * WR + l0 / TPR;
-        float va, vb;
-        refs_of(l0, d, va, vb);
-        const float sc = scale_of(va, vb);
-        const uint32_t ka = f2key(va), kb = f2key(vb);
-        uint32_t prefix = 0;
-        int k = a.rank;
-        for (int bit = 31; bit >= 0; --bit) {
-          const uint32_t hmask = bit == 31 ? 0u : ~((2u << bit) - 1u);
-          const bool za = oka && ((ka & hmask) == prefix) && !((ka >> bit) & 1u);
-          const bool zb = okb && ((kb & hmask) == prefix) && !((kb >> bit) & 1u);
-          const int c0 = __popcll(__ballot(za)) + __popcll(__ballot(zb));
-          if (k >= c0) {
-            k -= c0;
-            prefix |= 1u << bit;
+      // Pass 2: exact ranked value (k-th smallest) of each detection by a pivoting select on the
+      // bit patterns (cells are non-negative: unsigned order == value order), then the record
+      coop_rounds(detw, cnt + 8, list, aux, base + (uint32_t)dx, [&](int n) {
+        for (int j = wv; j < n; j += WPB) {
+          int trow, d;
+          cell_of(list[j], trow, d);
+          const uint32_t slot = aux[j];
+          float va, vb;
+          refs_of(trow, d, va, vb);
+          const float sc = scale_of(va, vb);
+          uint32_t ranked = 0;
+#ifdef FMCW_CFAR2D_ABLATE
+          if (FMCW_CFAR2D_ABLATE != 2)
+#endif
+          ranked = wave_select_kth(oka ? __float_as_uint(va) : 0u, okb ? __float_as_uint(vb) : 0u,
+                                   __ballot(oka), __ballot(okb), a.rank);
+          if (lane == 0 && slot < sink.cap) {
+            fmcw_det dd;
+            dd.frame = (uint32_t)(frame0 + f);
+            dd.range = (uint16_t)(r0 + trow);
+            dd.doppler = (uint16_t)d;
+            dd.mag = rr.row(trow + a.hr)[midx(d)];
+            dd.threshold = sc * __uint_as_float(ranked);
+            sink.scratch[slot] = dd;
           }
         }
-        const uint32_t slot = base + o;
-        if (lane == 0 && slot < sink.cap) {
-          fmcw_det dd;
-          dd.frame = (uint32_t)(frame0 + f);
-          dd.range = (uint16_t)(r0 + rl);
-          dd.doppler = (uint16_t)d;
-          dd.mag = tile[(rl + a.hr) * RS + midx(d)];
-          dd.threshold = sc * key2f(prefix);
-          sink.scratch[slot] = dd;
-        }
-        ++o;
-      }
-    }
-  }
+      });
+    }  // steps
+  }    // strips
 }

@@ -87,6 +87,7 @@ struct fmcw_handle {
   size_t cfar2d_smem = 0;
   // two-stream chunk pipeline (K1 of chunk c + 1 beside K2 of chunk c, fmcw_enqueue)
   int pipe_nb = 0;                      // intermediate buffers in the ring (0 = serial chunks)
+  int cfar2_steps = 0;                  // 2-D CFAR steps per strip (0 = cost model; FMCW_CFAR2D_STEPS)
   float2* inter_b[3] = {nullptr, nullptr, nullptr};
   float* lin_b[3] = {nullptr, nullptr, nullptr};
   hipStream_t ps[2] = {nullptr, nullptr};
@@ -167,7 +168,7 @@ Cfar1Fn cfar1_fn(uint32_t nc) {
   return nullptr;
 }
 
-using Cfar2Fn = void (*)(const float*, int, int, int, int, Cfar2DArgs, DetSink);
+using Cfar2Fn = void (*)(const float*, int, int, int, int, int, Cfar2DArgs, DetSink);
 struct Cfar2Info {
   Cfar2Fn fn;
   int TR;
@@ -400,6 +401,27 @@ size_t tiles_per_frame(const fmcw_handle* h) {
   return c.n_range / doppler_info(c.n_doppler).WR;
 }
 
+// Steps per 2-D CFAR strip.  A strip of S steps loads S*TR + 2*hr rows for S*TR CUT rows; the
+// workgroups run ceil(strips / grid) rounds.  Cost model per round, in units of one step's
+// compute: S * (1 + 0.5) (a step's TR new rows cost about half its compute) + 0.5 * 2hr / TR for
+// the halo rows a strip loads once.  Longer strips: less halo traffic, fewer strips to spread.
+int cfar2_steps_model(int nf, int tpf, int grid, int tr, int hr) {
+  int best = 1;
+  double best_cost = 1e300;
+  for (int S = 1; S <= std::min(32, tpf); ++S) {
+    const long strips = (long)nf * ((tpf + S - 1) / S);
+    const long rounds = (strips + grid - 1) / std::max(1, grid);
+    const double cost = (double)rounds * (1.5 * S + (double)hr / tr);
+    if (cost < best_cost - 1e-9) {
+      best_cost = cost;
+      best = S;
+    }
+  }
+  return best;
+}
+
+constexpr size_t kCfar2Batch = 16;  // frames per 2-D CFAR launch on the caller's map (at least)
+
 // The CFAR launcher shared by fmcw_enqueue (map just produced by K2) and fmcw_cfar.
 int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipStream_t s) {
   const fmcw_config& c = h->cfg;
@@ -408,12 +430,15 @@ int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipS
   if (c.cfar_kind == FMCW_CFAR_OS2D) {
     const Cfar2DArgs a = cfar2_args(c);
     const Cfar2Info ci = cfar2_info(c.n_doppler, a.hd, a.gd);
-    // workgroup tiles: 4 consecutive wave tiles of one frame
-    const int n_wg_tiles = nf * (int)((tiles_per_frame(h) + 3) / 4);
-    const int grid = std::min(n_wg_tiles, h->grid_cfar);
+    // workgroup tiles (steps): 4 consecutive wave tiles of one frame; a strip is `steps` of them
+    const int tpf = (int)((tiles_per_frame(h) + 3) / 4);
+    const int steps = h->cfar2_steps ? std::min(h->cfar2_steps, tpf)
+                                     : cfar2_steps_model(nf, tpf, h->grid_cfar, doppler_info(c.n_doppler).WR * 4, a.hr);
+    const int n_strips = nf * ((tpf + steps - 1) / steps);
+    const int grid = std::min(n_strips, h->grid_cfar);
     ProfScope ps(h, FMCW_K_CFAR2D, s);
     hipLaunchKernelGGL(ci.fn, dim3(grid), dim3(256), h->cfar2d_smem, s, map_chunk, (int)c.n_range,
-                       n_wg_tiles, frame0, tile0, a, sink);
+                       n_strips, steps, frame0, tile0, a, sink);
     return check_launch("k_cfar2d");
   }
   // 1-D on a caller map (fmcw_cfar); inside fmcw_enqueue the 1-D CFAR is fused into K2
@@ -621,6 +646,7 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   const size_t frame_inter = (size_t)c.n_rx * c.n_range * c.n_doppler * sizeof(float2);
   // two-stream pipeline of chunks (FMCW_PIPE=1): ring of FMCW_PIPE_BUFS intermediate buffers of
   // FMCW_PIPE_CHUNK frames, sized so the ring stays in the 256 MiB Infinity Cache
+  if (const char* cs = std::getenv("FMCW_CFAR2D_STEPS")) h->cfar2_steps = std::max(0, std::atoi(cs));
   const char* pe = std::getenv("FMCW_PIPE");
   const bool pipe = pe && pe[0] == '1';
   if (pipe) {
@@ -803,8 +829,8 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
       if ((rc = check_launch("k_fused"))) return rc;
     }
     if (c.cfar_kind == FMCW_CFAR_OS2D)
-      for (size_t f0 = 0; f0 < n_frames; f0 += h->chunk) {
-        const int nf = (int)std::min<size_t>(h->chunk, n_frames - f0);
+      for (size_t f0 = 0; f0 < n_frames; f0 += std::max<size_t>(h->chunk, kCfar2Batch)) {
+        const int nf = (int)std::min<size_t>(std::max<size_t>(h->chunk, kCfar2Batch), n_frames - f0);
         if ((rc = launch_cfar(h, rd_map + f0 * frame_px, nf, (int)f0, s))) return rc;
       }
     if (c.cfar_kind != FMCW_CFAR_NONE) return launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, s);
@@ -825,6 +851,7 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
     HIP_TRY(hipStreamWaitEvent(sa, h->ev_fork, 0));
     HIP_TRY(hipStreamWaitEvent(sb, h->ev_fork, 0));
   }
+  size_t k3_f0 = 0;  // first frame of the caller's map not yet through the 2-D CFAR
   for (size_t ci = 0; ci < n_chunks; ++ci) {
     const size_t f0 = ci * h->chunk;
     const int nf = (int)std::min<size_t>(h->chunk, n_frames - f0);
@@ -862,7 +889,15 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
     }
     if (piped) HIP_TRY(hipEventRecord(h->ev_free[b], sb));
     if (c.cfar_kind == FMCW_CFAR_OS2D) {
-      if ((rc = launch_cfar(h, lin, nf, (int)f0, sb))) return rc;
+      // on the caller's map the 2-D CFAR runs over batches of >= kCfar2Batch frames: its
+      // strips then cover more rows per workgroup and more frames share one launch
+      const size_t done = f0 + (size_t)nf;
+      if (!(rd_map && c.map_kind == FMCW_MAP_LINEAR)) {  // chunk scratch: this chunk only
+        if ((rc = launch_cfar(h, lin, nf, (int)f0, sb))) return rc;
+      } else if (done - k3_f0 >= kCfar2Batch || done == n_frames) {
+        if ((rc = launch_cfar(h, rd_map + k3_f0 * frame_px, (int)(done - k3_f0), (int)k3_f0, sb))) return rc;
+        k3_f0 = done;
+      }
     }
   }
   if (piped) {  // join: everything on ps[0] precedes ps[1]'s last K2, so ps[1] alone is enough

@@ -437,3 +437,19 @@ def test_repeated_launches_and_device_pointers(monkeypatch, env):
         n, _ = (int(v) for v in dn.download(np.uint32, (2,)))
         np.testing.assert_array_equal(dmap.download(np.float32, (F, ns, nc)), m0)
         np.testing.assert_array_equal(ddet.download(DET_DTYPE, (n,)), d0)
+
+
+@pytest.mark.parametrize("steps", ["1", "3", "7", "0"])
+def test_cfar2d_strips_and_batched_launches(monkeypatch, steps):
+    """The 2-D CFAR walks strips of `steps` workgroup tiles through a ring of staged rows
+    (cfar2d.hpp RowRing; 3 and 7 leave a short last strip per frame) and, on the caller's map,
+    runs once per >= 16 frames (20 frames in chunks of 4: launches of 16 + 4).  Detections
+    bit-exact vs the C oracle on the map the path wrote."""
+    monkeypatch.setenv("FMCW_CFAR2D_STEPS", steps)
+    ns, nc, nf = 512, 128, 20
+    cube = synth.frames(nf, ns, nc, 1, "two_targets")
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os2d", max_frames=nf, chunk_frames=4) as core:
+        out = core.process(cube)
+    want = CB.cfar(out.rd_map, O.Cfar2D(), threads=16)
+    np.testing.assert_array_equal(out.dets, want)
+    assert out.n_dets > nf
