@@ -132,16 +132,24 @@ __device__ __forceinline__ uint32_t cfar2d_screen(const RowRing& rr, int rl, int
   return bits;
 }
 
-// The same pair screen on packed 16-bit keys, two CUTs per VALU op.  The key of a cell is the
-// high half of its bit pattern (cells are non-negative: sign 0, 8 exponent and 7 mantissa
-// bits), monotone in the value, so min() commutes with it.  Each CUT gets the key of
-// q = fl(cut / s_min) + 8 ulps (cut * fl(1 / s_min): <= 2 ulps of error), and a pair counts
-// only if its min key is STRICTLY above that key: then min > q > cut / s_min in reals, so both
-// refs have s_min * ref > cut and fl(s_min * ref) >= cut -- still a lower bound on the exact
-// count (the key's 2^-7 resolution only makes the screen a little weaker).  Per window row:
-// 27 byte-perms build hi16 pairs, 26 v_pk_min_u16 the packed pair minima, and each
-// (two CUTs, one pair) step is v_pk_sub_u16 + v_pk_lshrrev_b16 + v_pk_add_u16 (bit 15 of
-// pairmin - (key + 1) is set iff pairmin <= key).  No multiplies in the row loop.
+// Phase A screen on packed 16-bit keys, two CUTs per VALU op, over disjoint PAIRS of
+// Doppler-adjacent references.  A pair whose MAX satisfies fl(s_min * max) >= cut holds at
+// least one reference that does, so #{such pairs} is a lower bound on the exact count
+// E(s_min) = #{fl(s_min * ref) >= cut}; a cell whose bound reaches n_ref - k cannot detect at
+// any admissible scale.  (The max bound beats 2 * #{pairs whose min qualifies} exactly where it
+// matters: for a reference exceeding the cut's level with probability p it rejects from
+// p ~ 0.32 instead of p ~ 0.52; on single-channel Rayleigh maps 1.9 % of the cells survive it
+// instead of 4.8 %.)  A reference row of 2 HD + 1 cells gives HD pairs (its last cell is left
+// out), a guard row two segments of HD - GD cells, (HD - GD) / 2 pairs each.
+// The key of a cell is the high half of its bit pattern (cells are non-negative: sign 0, 8
+// exponent and 7 mantissa bits), monotone in the value, so max() commutes with it.  Each CUT
+// gets the key of q = fl(cut / s_min) + 8 ulps (cut * fl(1 / s_min): <= 2 ulps of error), and
+// a pair counts only if its max key is STRICTLY above that key: then max > q > cut / s_min in
+// reals, so s_min * max > cut and fl(s_min * max) >= cut (the key's 2^-7 resolution only makes
+// the screen a little weaker).  Per window row: 27 byte-perms build hi16 pairs, 26
+// v_pk_max_u16 the packed pair maxima, and each (two CUTs, one pair) step is v_pk_sub_u16 +
+// v_pk_lshrrev_b16 + v_pk_add_u16 (bit 15 of pairmax - (key + 1) is set iff pairmax <= key).
+// The survivors are then counted exactly, one per lane.
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 template <int NC, int HD, int GD>
@@ -169,7 +177,7 @@ __device__ __forceinline__ uint32_t cfar2d_screen16(const RowRing& rr, int rl, i
   for (int dr = -a.hr; dr <= a.hr; ++dr) {
     float v[4 * NV];
     load_cells<NV>(rr.row(rl + a.hr + dr) + midx(d0), O0, v);
-    u16x2 P[W - 2];  // P[k] = (pairmin key k, pairmin key k + 1), cell 0 = d0 - HD
+    u16x2 P[W - 2];  // P[k] = (pairmax key k, pairmax key k + 1), cell 0 = d0 - HD
     {
       uint32_t V[W - 1];  // V[k] = (key of cell k, key of cell k + 1)
 #pragma unroll
@@ -178,7 +186,7 @@ __device__ __forceinline__ uint32_t cfar2d_screen16(const RowRing& rr, int rl, i
                                      0x07060302u);
 #pragma unroll
       for (int k = 0; k < W - 2; ++k)
-        P[k] = __builtin_elementwise_min(__builtin_bit_cast(u16x2, V[k]), __builtin_bit_cast(u16x2, V[k + 1]));
+        P[k] = __builtin_elementwise_max(__builtin_bit_cast(u16x2, V[k]), __builtin_bit_cast(u16x2, V[k + 1]));
     }
     if (dr >= -a.gr && dr <= a.gr) {  // guard row (uniform branch)
 #pragma unroll
@@ -200,32 +208,38 @@ __device__ __forceinline__ uint32_t cfar2d_screen16(const RowRing& rr, int rl, i
   uint32_t bits = 0;
 #pragma unroll
   for (int p = 0; p < 8; ++p) {
-    bits |= (2 * (np - (int)nlt[p].x) < need ? 1u : 0u) << (2 * p);
-    bits |= (2 * (np - (int)nlt[p].y) < need ? 1u : 0u) << (2 * p + 1);
+    bits |= (np - (int)nlt[p].x < need ? 1u : 0u) << (2 * p);
+    bits |= (np - (int)nlt[p].y < need ? 1u : 0u) << (2 * p + 1);
   }
   return bits;
 }
 
-// Exact candidate test of one cell (CUT row rl of the group tile, Doppler d), one lane per
-// cell.  With E(s) = #{fl(s * ref) >= cut}, the cell can only detect if E(s) < need for the
-// scale s it gets.  E(s_min) >= need rules every scale out.  The scale is sc_min only when
-// #{ref < mean / 2} >= rank + 1 (os_cfar_2d.vhd:195-199); otherwise it is >= s2 =
-// min(sc_nom, sc_max) and E(s2) >= need rules the cell out too.  #{ref < mean / 2} is bounded
-// from above with any-order fp32 sum x (1 + 2^-15) (the sum of <= 128 non-negative terms in
-// another order differs by < 2^-16 relative; compat's integer sums are exact), so the test
-// keeps every cell that can detect.  On single-channel (Rayleigh) maps it drops ~99 % of the
-// cells E(s_min) alone passes.  Addresses: midx(d + dd) with a runtime d.
+// Candidate test of one screen survivor (CUT row rl of the group tile, Doppler d), one lane per
+// cell; it keeps every cell that can detect.  With E(s) = #{fl(s * ref) >= cut}, the cell can
+// only detect if E(s) < need for the scale s it gets.  E(s_min) >= need rules every scale out.
+// The scale is sc_min only when #{ref < mean / 2} >= rank + 1 (os_cfar_2d.vhd:195-199);
+// otherwise it is >= s2 = min(sc_nom, sc_max) and E(s2) >= need rules the cell out too.
+// E(s_min) and E(s2) are bounded from below with the screen's 16-bit keys, both in one packed
+// op per reference (a reference counts if its key is strictly above key(cut / s) + 8 ulps), and
+// #{ref < mean / 2} from above with an any-order fp32 sum x (1 + 2^-15) (the sum of <= 128
+// non-negative terms in another order differs by < 2^-16 relative; compat's integer sums are
+// exact).  On single-channel (Rayleigh) maps this leaves ~0.3 % of the cells E(s_min) alone
+// would pass.  Addresses: midx(d + dd) with a runtime d.
 template <int NC, int HD, int GD>
-__device__ __forceinline__ bool cfar2d_exact_a(const RowRing& rr, int rl, int d, const Cfar2DArgs& a, int need) {
+__device__ __forceinline__ bool cfar2d_exact_a(const RowRing& rr, int rl, int d, const Cfar2DArgs& a, int need,
+                                               int sub, int L) {
   const float* crow = rr.row(rl + a.hr);
   const int x = d + MH;
   auto at = [&](const float* row, int dd) { return row[(x + dd) + (((x + dd) >> 4) << 2)]; };
-  const uint32_t cbits = __float_as_uint(at(crow, 0));
+  const float cut = at(crow, 0);
   const float s2 = a.override_ ? a.s_min : fminf(a.sc_nom, a.sc_max);
-  uint32_t lt = 0, lt2 = 0;
+  const uint32_t k1 = min((__float_as_uint(cut * (1.0f / a.s_min)) + 8u) >> 16, 0x7fffu) + 1u;
+  const uint32_t k2 = min((__float_as_uint(cut * (1.0f / s2)) + 8u) >> 16, 0x7fffu) + 1u;
+  const u16x2 kk = __builtin_bit_cast(u16x2, k1 | (k2 << 16));
+  u16x2 nlt = (u16x2)(0);  // #{refs not counted} for (s_min, s2)
   float sum = 0.f;
-  auto visit = [&](auto&& fn) {
-    for (int dr = -a.hr; dr <= a.hr; ++dr) {
+  auto visit = [&](auto&& fn) {  // this lane's rows: dr = -hr + sub, every L-th
+    for (int dr = -a.hr + sub; dr <= a.hr; dr += L) {
       const float* row = rr.row(rl + a.hr + dr);
       if (dr >= -a.gr && dr <= a.gr) {
 #pragma unroll
@@ -238,16 +252,21 @@ __device__ __forceinline__ bool cfar2d_exact_a(const RowRing& rr, int rl, int d,
     }
   };
   visit([&](float v) {
-    lt += lt_bit(__float_as_uint(a.s_min * v), cbits);
-    lt2 += lt_bit(__float_as_uint(s2 * v), cbits);
+    const uint32_t kv = __builtin_amdgcn_perm(__float_as_uint(v), __float_as_uint(v), 0x07060302u);
+    nlt += (u16x2)(__builtin_bit_cast(u16x2, kv) - kk) >> (unsigned short)15;
     sum += v;
   });
-  if ((int)lt <= a.n_ref - need) return false;                // E(s_min) >= need
-  if ((int)lt2 > a.n_ref - need || a.override_) return true;  // E(s2) < need
+  for (int x = 1; x < L; x <<= 1) {  // the cell's L lanes are adjacent and aligned
+    nlt += __builtin_bit_cast(u16x2, __shfl_xor(__builtin_bit_cast(int, nlt), x, 64));
+    sum += __shfl_xor(sum, x, 64);
+  }
+  if (a.n_ref - (int)nlt.x >= need) return false;                // E(s_min) >= need
+  if (a.n_ref - (int)nlt.y < need || a.override_) return true;   // E(s2) may be < need
   const float half_up = sum * (1.0f + 1.0f / 32768.0f) / (float)a.n_ref * 0.5f;
-  uint32_t n_lo = 0;
-  visit([&](float v) { n_lo += v < half_up ? 1u : 0u; });
-  return (int)n_lo >= a.rank + 1;                             // sc_min still possible
+  int n_lo = 0;
+  visit([&](float v) { n_lo += v < half_up ? 1 : 0; });
+  for (int x = 1; x < L; x <<= 1) n_lo += __shfl_xor(n_lo, x, 64);
+  return n_lo >= a.rank + 1;                                     // sc_min still possible
 }
 
 // Phase A for a compile-time Doppler extent HD / guard GD; returns this lane's candidate bits.
@@ -526,17 +545,25 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
         trow = we * WR + le / TPR;
         d = (le % TPR) * 16 + (int)(e & 15u);
       };
+#ifdef FMCW_CFAR2D_ABLATE
+      if (FMCW_CFAR2D_ABLATE != 4)
+#endif
       if constexpr (HD > 0 && FMCW_CFAR2D_SCREEN) {
-        // survivors of the screen -> exact count, one lane per cell, 256 per round over the
-        // whole workgroup (a hot tile's survivors spread over all four waves)
+        // survivors of the screen -> candidate test, 256 per round over the whole workgroup (a
+        // hot tile's survivors spread over all four waves).  A round of <= 32 / 64 / 128 cells
+        // gives each cell 8 / 4 / 2 adjacent lanes that split its rows: a step usually has a
+        // few dozen survivors, and one lane walking all 128 references of a cell alone set the
+        // critical path of the step (config 5: 89 -> 71 us per frame).
         aux[threadIdx.x] = 0u;
         const uint32_t scr = cand;
         coop_rounds(scr, cnt, list, nullptr, 0u, [&](int n) {
-          if ((int)threadIdx.x < n) {
+          const int L = n <= 32 ? 8 : n <= 64 ? 4 : n <= 128 ? 2 : 1;
+          const int j = (int)threadIdx.x / L, sub = (int)threadIdx.x % L;
+          if (j < n) {  // whole aligned groups of L lanes
             int trow, d;
-            const uint32_t e = list[threadIdx.x];
+            const uint32_t e = list[j];
             cell_of(e, trow, d);
-            if (cfar2d_exact_a<NC, HD, GD>(rr, trow, d, a, need))
+            if (cfar2d_exact_a<NC, HD, GD>(rr, trow, d, a, need, sub, L) && sub == 0)
               atomicOr(&aux[e >> 4], 1u << (e & 15u));
           }
         });
@@ -587,6 +614,9 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
           refs_of(trow, d, va, vb);
           const float sc = scale_of(va, vb);
           const int n_ge = __popcll(__ballot(oka && sc * va >= cut)) + __popcll(__ballot(okb && sc * vb >= cut));
+#ifdef FMCW_CFAR2D_ABLATE  // 3 / 4: every candidate / screen survivor is reported (counting)
+          if (FMCW_CFAR2D_ABLATE >= 3 && lane == 0) atomicOr(&aux[e >> 4], 1u << (e & 15u));
+#endif
           if (n_ge < need && lane == 0) atomicOr(&aux[e >> 4], 1u << (e & 15u));
         }
       });

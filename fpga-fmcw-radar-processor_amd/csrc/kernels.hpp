@@ -798,6 +798,18 @@ __device__ __forceinline__ float2 q16c(float2 v) { return make_float2(sat16(rint
 #ifndef FMCW_K2_PREFETCH  // K2 (MTI off): points of the next (tile, rx) unit loaded ahead (0, 8 or 16)
 #define FMCW_K2_PREFETCH 16
 #endif
+#ifndef FMCW_K2_XCD       // K2: contiguous logical workgroup ids per XCD (1)
+#define FMCW_K2_XCD 1
+#endif
+// Workgroups are dispatched round-robin over the 8 XCDs (XCD = id % 8, MI355X_MICROARCH.md).
+// Giving each XCD a contiguous range of logical ids puts neighbouring tiles -- which read the
+// two halves of the same 128-B lines of the tiled spectrum when a workgroup covers only 64 B of
+// each 1 KiB tile (NC = 1024: 4 range rows x 16 B) -- behind the same L2.
+__device__ __forceinline__ int xcd_block_id(int bid, int grid) {
+  if (grid & 7) return bid;
+  return (bid & 7) * (grid >> 3) + (bid >> 3);
+}
+
 #ifndef FMCW_K2_ORDER     // K2 tile order (see k_doppler)
 #define FMCW_K2_ORDER 1
 #endif
@@ -899,9 +911,14 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
       }
     }
   };
-  prefetch(blockIdx.x * WPB + wv, 0);
+  // XCD-contiguous ids only where a workgroup reads less than a 128-B line of each tile
+  // (measured: config 5 K2 177 -> 110 us per 4 frames; configs 2 / 3, whose workgroups read
+  // whole lines, 2-3 % slower with it)
+  const bool xcd = FMCW_K2_XCD && ((WPB * WR * 8) << lgT) < 128;
+  const int bid = xcd ? xcd_block_id((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+  prefetch(bid * WPB + wv, 0);
 
-  for (int tile = blockIdx.x * WPB + wv; tile < n_tiles; tile += tile_step) {
+  for (int tile = bid * WPB + wv; tile < n_tiles; tile += tile_step) {
     const int t = opaque(t0);
     float2* buf = wreg + rr * REGD;
     // frame-minor order: consecutive tiles are the same rows of consecutive frames, so the

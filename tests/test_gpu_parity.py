@@ -93,6 +93,7 @@ def test_magnitude_kat_gpu(gpu):
     (1024, 128, 1, "i16", 2),     # reference core N_RANGE x N_DOPPLER, ADC ints
     (4096, 64, 2, "f32", 1),
     (8192, 32, 1, "f16", 1),      # largest range FFT, fp16 samples
+    (8192, 64, 2, "i16", 2),      # largest range FFT over several groups, frames and rx
     (64, 32, 1, "f32", 4),        # smallest
     (128, 64, 1, "i16", 2),
     (512, 64, 1, "f32", 2),
@@ -115,7 +116,7 @@ def test_range_ct_parity(gpu, ns, nc, nrx, dtype, nf):
             assert rel_err(got[f, rx], ref[f, rx]) <= MAP_TOL
 
 
-@pytest.mark.parametrize("ns,nc", [(1024, 128), (256, 32), (4096, 32)])
+@pytest.mark.parametrize("ns,nc", [(1024, 128), (256, 32), (4096, 32), (8192, 32)])
 def test_range_ct_q15_rtl(gpu, ns, nc):
     """RTL-compat integer window (FMCW_WIN_Q15_RTL) on full-range int16 words, saturation
     included, vs the oracle's window_q15_rtl (pinned to the ROM fixture) + fp64 FFT."""

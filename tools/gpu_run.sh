@@ -41,6 +41,8 @@ for s in "$@"; do
         FMCW_LIB="$PWD/$lib" run "cfar2d_${v#var_}" 300 python tools/cfar2d_bench.py ${CFAR2D_ARGS:-}
       done ;;
     gpu_cfar_tests) run pytest_cfar 600 python -u -m pytest tests -m gpu -v -x -k "cfar or 2d or os2d or config5 or c5 or tb" --timeout 170 --timeout-method thread -p no:cacheprovider ;;
+    pmcf_c*) w=${s#pmcf_}; run "pmcf_$w" 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmcf_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
+    pmcw_c*) w=${s#pmcw_}; run "pmcw_$w" 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcw_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
     counters) run counters 120 rocprofv3 -L ;;
     prof_c*) w=${s#prof_}; run "rocprof_stats_$w" 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 5 --warmup 2 --no-cpu-baseline --no-h2d ;;
     pmcsq_c*) w=${s#pmcsq_}; run "pmcsq_$w" 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/pmcsq_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
