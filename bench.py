@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--gather", default="rccl", choices=["rccl", "torch"],
                     help="N > 1: libfmcw's RCCL gather-to-root (no host sync) or torch all_gather")
     ap.add_argument("--no-h2d", action="store_true", help="skip the H2D-inclusive measurement")
+    ap.add_argument("--spectrum", default="f32", choices=["f32", "f16"],
+                    help="element type of the corner-turned spectrum (fmcw.h fmcw_spectrum_dtype)")
     return ap.parse_args()
 
 
@@ -88,7 +90,7 @@ def main():
             dist.init_process_group(backend)
 
     core = RadarCore(N_RANGE=ns, N_DOPPLER=nc, N_RX=nrx, in_dtype=wl["dtype"], cfar=wl["cfar"],
-                     max_frames=F, chunk_frames=args.chunk, device=local)
+                     max_frames=F, chunk_frames=args.chunk, device=local, spectrum=args.spectrum)
     # synthetic input: 16 distinct frames (seed 1234 + global frame), tiled to F, resident in HBM
     n_u = min(16, F)
     first_global = rank * F
@@ -205,8 +207,9 @@ def main():
     px = ns * nc * nrx
     ms_r, n_r = kt["k_range"]
     ms_d, n_d = kt["k_doppler"]
-    bytes_range = F * args.steps * px * (b_in + 8)                 # stage A: cube in + spectrum out
-    bytes_dopp = F * args.steps * (px * 8 + ns * nc * 4)           # spectrum in + map out
+    b_sp = 4 if args.spectrum == "f16" else 8                       # corner-turned spectrum element
+    bytes_range = F * args.steps * px * (b_in + b_sp)              # stage A: cube in + spectrum out
+    bytes_dopp = F * args.steps * (px * b_sp + ns * nc * 4)        # spectrum in + map out
     kern = {}
     for name, (ms, n) in kt.items():
         if n:
@@ -340,6 +343,7 @@ def main():
         "data": "synthetic (tb_radar_core-style point targets + uniform noise, int16-quantised)",
         "config": {"workload": wl["desc"], "frames_per_gpu_step": F, "n_chirps": nc,
                    "n_samples": ns, "n_rx": nrx, "cfar": wl["cfar"], "rd_map": "linear fp32, written",
+                   "spectrum": args.spectrum,
                    "detection_gather": gather_kind if gather else "none (single GPU)",
                    "parallelism": f"frame-sharded x{world}"},
         "e2e_GBps_algorithmic": round(e2e_bytes * args.steps * world / elapsed / 1e9, 1),

@@ -87,6 +87,7 @@ struct fmcw_handle {
   size_t cfar2d_smem = 0;
   // two-stream chunk pipeline (K1 of chunk c + 1 beside K2 of chunk c, fmcw_enqueue)
   int pipe_nb = 0;                      // intermediate buffers in the ring (0 = serial chunks)
+  size_t inter_bytes = 0;               // h->inter (chunk frames of the K1 -> K2 spectrum)
   int cfar2_steps = 0;                  // 2-D CFAR steps per strip (0 = cost model; FMCW_CFAR2D_STEPS)
   float2* inter_b[3] = {nullptr, nullptr, nullptr};
   float* lin_b[3] = {nullptr, nullptr, nullptr};
@@ -114,14 +115,18 @@ namespace {
 // ---- kernel dispatch tables ------------------------------------------------------------
 using RangeFn = void (*)(const void*, float2*, const float*, const float*, int, int, float);
 
-template <int N>
-RangeFn range_fn(int dtype, bool q15) {
+template <int N, bool H16>
+RangeFn range_fn_t(int dtype, bool q15) {
   switch (dtype) {
-    case FMCW_IN_F32: return k_range<N, LoadF32>;
-    case FMCW_IN_F16: return k_range<N, LoadF16>;
-    case FMCW_IN_I16: return q15 ? k_range<N, LoadI16, true> : k_range<N, LoadI16>;
+    case FMCW_IN_F32: return k_range<N, LoadF32, false, H16>;
+    case FMCW_IN_F16: return k_range<N, LoadF16, false, H16>;
+    case FMCW_IN_I16: return q15 ? k_range<N, LoadI16, true, H16> : k_range<N, LoadI16, false, H16>;
   }
   return nullptr;
+}
+template <int N>
+RangeFn range_fn(int dtype, bool q15, bool h16) {
+  return h16 ? range_fn_t<N, true>(dtype, q15) : range_fn_t<N, false>(dtype, q15);
 }
 
 struct RangeInfo {
@@ -129,10 +134,10 @@ struct RangeInfo {
   int T, RB, NT;
 };
 
-RangeInfo range_info(uint32_t n, int dtype, int window = FMCW_WIN_HAMMING) {
+RangeInfo range_info(uint32_t n, int dtype, int window = FMCW_WIN_HAMMING, bool h16 = false) {
   const bool q15 = window == FMCW_WIN_Q15_RTL;
   switch (n) {
-#define R_(N) case N: return {range_fn<N>(dtype, q15), RangeGeom<N>::T, RangeGeom<N>::RB, RangeGeom<N>::NT};
+#define R_(N) case N: return {range_fn<N>(dtype, q15, h16), RangeGeom<N>::T, RangeGeom<N>::RB, RangeGeom<N>::NT};
     R_(64) R_(128) R_(256) R_(512) R_(1024) R_(2048) R_(4096) R_(8192)
 #undef R_
   }
@@ -145,13 +150,19 @@ struct DopplerInfo {
   DopplerFn fn;
   int WR, NT;  // range rows per wave tile, threads per workgroup (DopplerGeom::WPB tiles)
 };
-template <int N>
-DopplerFn doppler_fn(int mti) {
-  return mti == FMCW_MTI_2PULSE ? k_doppler<N, 2> : mti == FMCW_MTI_3PULSE ? k_doppler<N, 3> : k_doppler<N, 0>;
+template <int N, bool H16>
+DopplerFn doppler_fn_t(int mti) {
+  return mti == FMCW_MTI_2PULSE   ? k_doppler<N, 2, H16>
+         : mti == FMCW_MTI_3PULSE ? k_doppler<N, 3, H16>
+                                  : k_doppler<N, 0, H16>;
 }
-DopplerInfo doppler_info(uint32_t nc, int mti = FMCW_MTI_OFF) {
+template <int N>
+DopplerFn doppler_fn(int mti, bool h16) {
+  return h16 ? doppler_fn_t<N, true>(mti) : doppler_fn_t<N, false>(mti);
+}
+DopplerInfo doppler_info(uint32_t nc, int mti = FMCW_MTI_OFF, bool h16 = false) {
   switch (nc) {
-#define D_(N) case N: return {doppler_fn<N>(mti), DopplerGeom<N>::WR, DopplerGeom<N>::NT};
+#define D_(N) case N: return {doppler_fn<N>(mti, h16), DopplerGeom<N>::WR, DopplerGeom<N>::NT};
     D_(32) D_(64) D_(128) D_(256) D_(512) D_(1024)
 #undef D_
   }
@@ -308,6 +319,10 @@ int validate(const fmcw_config& c) {
   if ((c.compat_rtl & FMCW_COMPAT_MTI) && c.mti_mode == FMCW_MTI_OFF)
     return fail(FMCW_EINVAL, "compat MTI needs mti_mode 2 or 3");
   if (c.range_shift > 13) return fail(FMCW_EINVAL, "range_shift=%u: must be in [0, 13]", c.range_shift);
+  if (c.spectrum_dtype != FMCW_SPEC_F32 && c.spectrum_dtype != FMCW_SPEC_F16)
+    return fail(FMCW_EINVAL, "spectrum_dtype=%d unknown", c.spectrum_dtype);
+  if (c.spectrum_dtype == FMCW_SPEC_F16 && (c.compat_rtl & FMCW_COMPAT_MTI))
+    return fail(FMCW_EINVAL, "compat MTI is defined on the fp32 spectrum (spectrum_dtype F16)");
   return FMCW_OK;
 }
 
@@ -519,7 +534,9 @@ void setup_fused(fmcw_handle* h) {
   // opt-in (FMCW_FUSED=1): measured slower than the K1/K2 pipeline at config 2
   const char* env = std::getenv("FMCW_FUSED");
   if (!env || env[0] != '1') return;
-  if (c.n_rx != 1 || c.mti_mode != FMCW_MTI_OFF || c.window == FMCW_WIN_Q15_RTL) return;
+  if (c.n_rx != 1 || c.mti_mode != FMCW_MTI_OFF || c.window == FMCW_WIN_Q15_RTL ||
+      c.spectrum_dtype != FMCW_SPEC_F32)
+    return;
   if (h->n_cu % 8 != 0) return;
   const FusedInfo fi = fused_info(c.n_range, c.n_doppler, c.in_dtype);
   if (!fi.fn) return;
@@ -638,12 +655,13 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   h->cfg = *cfg;
   const fmcw_config& c = h->cfg;
   h->n_cu = prop.multiProcessorCount;
-  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window);
+  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, c.spectrum_dtype == FMCW_SPEC_F16);
   h->T = ri.T;
   h->RB = ri.RB;
   h->lgT = __builtin_ctz(ri.T);
   h->lgRB = __builtin_ctz(ri.RB);
-  const size_t frame_inter = (size_t)c.n_rx * c.n_range * c.n_doppler * sizeof(float2);
+  const size_t frame_inter = (size_t)c.n_rx * c.n_range * c.n_doppler *
+                             (c.spectrum_dtype == FMCW_SPEC_F16 ? sizeof(uint32_t) : sizeof(float2));
   // two-stream pipeline of chunks (FMCW_PIPE=1): ring of FMCW_PIPE_BUFS intermediate buffers of
   // FMCW_PIPE_CHUNK frames, sized so the ring stays in the 256 MiB Infinity Cache
   if (const char* cs = std::getenv("FMCW_CFAR2D_STEPS")) h->cfar2_steps = std::max(0, std::atoi(cs));
@@ -676,7 +694,9 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   } while (0)
   ALLOC(h->win_r, c.n_range * sizeof(float));
   ALLOC(h->win_d, c.n_doppler * sizeof(float));
-  ALLOC(h->inter, h->chunk * frame_inter);
+  // >= one fp32 frame: fmcw_range_ct writes the fp32 spectrum through it whatever spectrum_dtype
+  h->inter_bytes = std::max(h->chunk * frame_inter, (size_t)c.n_rx * c.n_range * c.n_doppler * sizeof(float2));
+  ALLOC(h->inter, h->inter_bytes);
   if (c.cfar_kind == FMCW_CFAR_OS2D) ALLOC(h->lin_scratch, (size_t)h->chunk * c.n_range * c.n_doppler * sizeof(float));
   if (h->pipe_nb) {
     h->inter_b[0] = h->inter;
@@ -732,7 +752,7 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
 #ifdef FMCW_K1_GRID_PER_CU  // tuning switch (tools/build_variants.sh): K1 workgroups per CU
   h->grid_range = std::min(h->grid_range, FMCW_K1_GRID_PER_CU * h->n_cu);
 #endif
-  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode);
+  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype == FMCW_SPEC_F16);
   occupancy_grid(di.fn, di.NT, 0, h->n_cu, &h->grid_doppler);
   if (c.cfar_kind == FMCW_CFAR_OS2D) {
     const Cfar2DArgs a = cfar2_args(c);
@@ -787,8 +807,8 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
     return fail(FMCW_EINVAL, "n_dets_dev is required when a CFAR is configured");
   HIP_TRY(hipSetDevice(c.device_id));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window);
-  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode);
+  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, c.spectrum_dtype == FMCW_SPEC_F16);
+  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype == FMCW_SPEC_F16);
   const size_t frame_px = (size_t)c.n_range * c.n_doppler;
   const size_t in_frame_bytes = cube_bytes(c, 1);
   const Cfar1DArgs cf1 = cfar1_args(c);
@@ -973,11 +993,14 @@ int fmcw_range_ct(fmcw_handle* h, const void* cube, size_t n_frames, void* spec,
   if (n_frames < 1 || n_frames > c.max_frames) return fail(FMCW_EINVAL, "n_frames out of range");
   HIP_TRY(hipSetDevice(c.device_id));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window);
+  // the stage output is the fp32 spectrum whatever spectrum_dtype the path uses: K1's fp32
+  // variant, as many frames per launch as the intermediate buffer holds at 8 B per point
+  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, false);
   const size_t in_frame_bytes = cube_bytes(c, 1);
   const size_t fr_px = (size_t)c.n_rx * c.n_range * c.n_doppler;
-  for (size_t f0 = 0; f0 < n_frames; f0 += h->chunk) {
-    const int nf = (int)std::min<size_t>(h->chunk, n_frames - f0);
+  const size_t rc_chunk = std::max<size_t>(1, h->inter_bytes / (fr_px * sizeof(float2)));
+  for (size_t f0 = 0; f0 < n_frames; f0 += rc_chunk) {
+    const int nf = (int)std::min<size_t>(rc_chunk, n_frames - f0);
     const int n_groups = nf * (int)c.n_rx * (int)(c.n_doppler / ri.T);
     {
       ProfScope ps(h, FMCW_K_RANGE, s);

@@ -56,6 +56,26 @@ struct LoadI16 {
   }
 };
 
+// Corner-turned spectrum element: complex fp32 (8 B) or, with FMCW_SPEC_F16, a half2 (4 B)
+// holding X / N_range (|X| <= N max|x| would overflow fp16 for ADC-scale input; the 2^-log2 N
+// scale is exact and K2 undoes it at load).
+template <bool H16> struct SpecEl { using T = float2; };
+template <> struct SpecEl<true> { using T = uint32_t; };
+typedef _Float16 fmcw_h2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack_h2(float x, float y) {
+  return __builtin_bit_cast(uint32_t, fmcw_h2{(_Float16)x, (_Float16)y});
+}
+template <bool NT>
+__device__ __forceinline__ float2 ld_spec(const float2* p, float) { return ld_f2<NT>(p); }
+template <bool NT>
+__device__ __forceinline__ float2 ld_spec(const uint32_t* p, float scale) {
+  uint32_t u;
+  if constexpr (NT) u = __builtin_nontemporal_load(p);
+  else u = *p;
+  const fmcw_h2 h = __builtin_bit_cast(fmcw_h2, u);
+  return make_float2((float)h[0] * scale, (float)h[1] * scale);
+}
+
 // K1 geometry per range-FFT size: T chirps per workgroup, RB = 128/T (1 KiB chunks).
 template <int N> struct RangeGeom {
   static constexpr int P = N / 16;                   // threads per transform
@@ -79,7 +99,8 @@ template <int N> struct RangeGeom {
 // Q15 = RTL-compat integer range window (FMCW_WIN_Q15_RTL, int16 input): `win` then holds the
 // ROM integers c[n] (exact in fp32) and each sample is windowed as sat16((x c + 2^14) >> 14)
 // (window_multiplier.vhd:146-158) before it becomes fp32.
-template <int N, typename LD, bool Q15 = false>
+// H16 = FMCW_SPEC_F16: the tiles hold half2(X / N) (8-B stores of two chirps).
+template <int N, typename LD, bool Q15 = false, bool H16 = false>
 __global__ void __launch_bounds__(RangeGeom<N>::NT)
 __attribute__((amdgpu_waves_per_eu(FMCW_K1_WAVES > 0 && N < 8192 ? FMCW_K1_WAVES : 1)))
 k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* __restrict__ win,
@@ -116,7 +137,7 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
     const int t = opaque(t0);
     float2* buf = lds + q * REG;
     // Doppler window of this chirp folded in (K2 then skips it; FFT linearity), or 1
-    const float cw = chirp_w ? chirp_w[cb * T + q] : 1.f;
+    const float cw = (chirp_w ? chirp_w[cb * T + q] : 1.f) * (H16 ? 1.0f / N : 1.0f);
 
     // window coefficients for samples 2t + {0,1} + (N/8) m, re-read (L1/L2 hits) every group
     // rather than held: 16 VGPRs fewer across the LDS passes (the register peak)
@@ -165,7 +186,9 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
 
     // tiled corner turn: element (r, c) -> inter[rb][cb][RB][T]
     const float2* rd0 = lds + opaque(rd0_off);
-    float2* dst = inter + (size_t)fr * N * nc + ((size_t)chunk0 * ncb + cb) * (RB * T) + win0;
+    const size_t dbase = (size_t)fr * N * nc + ((size_t)chunk0 * ncb + cb) * (RB * T) + win0;
+    float2* dst = inter + dbase;
+    uint2* dst16 = reinterpret_cast<uint2*>(reinterpret_cast<uint32_t*>(inter) + dbase);
     const size_t dstep = (size_t)CI * ncb * (RB * T);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -177,7 +200,8 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
         v0 = lds[c0 * REG + pad16(r0 + i * (N / 8))];
         v1 = lds[(c0 + 1) * REG + pad16(r0 + i * (N / 8))];
       }
-      st_f4<FMCW_NT_SPEC_ST>(dst + i * dstep, make_float4(v0.x, v0.y, v1.x, v1.y));
+      if constexpr (H16) dst16[i * dstep / 2] = make_uint2(pack_h2(v0.x, v0.y), pack_h2(v1.x, v1.y));
+      else st_f4<FMCW_NT_SPEC_ST>(dst + i * dstep, make_float4(v0.x, v0.y, v1.x, v1.y));
     }
   }
 }
@@ -820,9 +844,9 @@ template <int NC, int MTI>
 constexpr int k2_waves() {
   return FMCW_K2_WAVES > 0 ? FMCW_K2_WAVES : (MTI == 0 && NC <= 256 && FMCW_K2_PREFETCH <= 8) ? 3 : 2;
 }
-template <int NC, int MTI>
+template <int NC, int MTI, bool H16 = false>
 __global__ void __launch_bounds__(DopplerGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(k2_waves<NC, MTI>())))
-k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int ns, int nrx,
+k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, int ns, int nrx,
           int lgT, int lgRB, int n_tiles, int frame0, int tile0, float* __restrict__ lin_map,
           float* __restrict__ db_map, int mag_mode, int mti_rtl, Cfar1DArgs cf, DetSink sink) {
   using Gm = DopplerGeom<NC>;
@@ -833,6 +857,9 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
 
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane0 = threadIdx.x & 63;
+  using SE = typename SpecEl<H16>::T;
+  const SE* const inter = reinterpret_cast<const SE*>(inter_in);
+  const float sscale = H16 ? (float)ns : 1.f;  // undoes K1's 1 / N_range of an fp16 spectrum
   const int rr = lane0 / P;
   const int t0 = lane0 % P;
   float* const mags = lds + wv * Gm::WFL;
@@ -879,7 +906,7 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
     }
   };
   const int tile_step = gridDim.x * WPB;
-  auto unit_src = [&](int tl, int rx) -> const float2* {
+  auto unit_src = [&](int tl, int rx) -> const SE* {
     int fu, lu;
     tile_fl(tl, fu, lu);
     const int ru = lu * WR + rr;
@@ -894,18 +921,18 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
   auto prefetch = [&](int tl, int rx) {
     if constexpr (PF) {
       if (tl < n_tiles) {
-        const float2* p = unit_src(tl, rx);
+        const SE* p = unit_src(tl, rx);
         const int tq = opaque(t0);
         if ((P & (T - 1)) == 0) {  // uniform: chirps t + P m sit a fixed S elements apart
-          const float2* pb = p + ((((uint32_t)tq >> lgT) << lgRB) << lgT) + ((uint32_t)tq & (uint32_t)(T - 1));
+          const SE* pb = p + ((((uint32_t)tq >> lgT) << lgRB) << lgT) + ((uint32_t)tq & (uint32_t)(T - 1));
           const uint32_t S = (uint32_t)(P >> lgT) << (lgRB + lgT);
 #pragma unroll
-          for (int m = 0; m < NPF; ++m) nxt[m] = ld_f2<FMCW_NT_SPEC_LD>(pb + (size_t)m * S);
+          for (int m = 0; m < NPF; ++m) nxt[m] = ld_spec<FMCW_NT_SPEC_LD>(pb + (size_t)m * S, sscale);
         } else {
 #pragma unroll
           for (int m = 0; m < NPF; ++m) {
             const uint32_t c = (uint32_t)(tq + P * m);
-            nxt[m] = ld_f2<FMCW_NT_SPEC_LD>(p + ((((c >> lgT) << lgRB) << lgT) | (c & (uint32_t)(T - 1))));
+            nxt[m] = ld_spec<FMCW_NT_SPEC_LD>(p + ((((c >> lgT) << lgRB) << lgT) | (c & (uint32_t)(T - 1))), sscale);
           }
         }
       }
@@ -936,8 +963,8 @@ k_doppler(const float2* __restrict__ inter, const float* __restrict__ win_d, int
       for (int m = 0; m < LR; ++m) acc[g][m] = 0.f;
 
     for (int rx = 0; rx < nrx; ++rx) {
-      const float2* src = inter + ((size_t)f * nrx + rx) * (size_t)ns * NC;
-      auto at = [&](uint32_t c) -> float2 { return ld_f2<FMCW_NT_SPEC_LD>(src + off_of(rbase, rin, c)); };
+      const SE* src = inter + ((size_t)f * nrx + rx) * (size_t)ns * NC;
+      auto at = [&](uint32_t c) -> float2 { return ld_spec<FMCW_NT_SPEC_LD>(src + off_of(rbase, rin, c), sscale); };
       float2 v[16];
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
@@ -1082,17 +1109,34 @@ k_det_scan_top(uint32_t* __restrict__ block_sum, int nb, uint32_t* __restrict__ 
   }
 }
 
+// One lane per tile; a tile with more than 8 detections (a target's row) is copied by the
+// whole wave, 64 records per step, so one hot tile does not serialise the kernel.
 __global__ void k_det_copy(const fmcw_det* __restrict__ scratch, uint32_t scratch_cap,
                            const uint32_t* __restrict__ wg_base, const uint32_t* __restrict__ wg_count,
                            const uint32_t* __restrict__ wg_off, const uint32_t* __restrict__ block_off,
                            int n, fmcw_det* __restrict__ out, uint32_t cap) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t c = wg_count[i];
-  if (!c) return;
-  const uint32_t b = wg_base[i], o = block_off[i >> 10] + wg_off[i];
-  for (uint32_t k = 0; k < c; ++k)
-    if (b + k < scratch_cap && o + k < cap) out[o + k] = scratch[b + k];
+  const int lane = threadIdx.x & 63;
+  uint32_t c = 0, b = 0, o = 0;
+  if (i < n) {
+    c = wg_count[i];
+    if (c) {
+      b = wg_base[i];
+      o = block_off[i >> 10] + wg_off[i];
+    }
+  }
+  if (c <= 8)
+    for (uint32_t k = 0; k < c; ++k)
+      if (b + k < scratch_cap && o + k < cap) out[o + k] = scratch[b + k];
+  uint64_t big = __ballot(c > 8);
+  while (big) {
+    const int l = __builtin_ctzll(big);
+    big &= big - 1;
+    const uint32_t cl = (uint32_t)__shfl((int)c, l, 64), bl = (uint32_t)__shfl((int)b, l, 64);
+    const uint32_t ol = (uint32_t)__shfl((int)o, l, 64);
+    for (uint32_t k = lane; k < cl; k += 64)
+      if (bl + k < scratch_cap && ol + k < cap) out[ol + k] = scratch[bl + k];
+  }
 }
 
 // --------------------------------------------------------------------------------------

@@ -24,6 +24,7 @@ MAP_LINEAR, MAP_DB = 1, 2
 CFAR_NONE, CFAR_OS1D, CFAR_OS2D = 0, 1, 2
 MTI_OFF, MTI_2PULSE, MTI_3PULSE = 0, 2, 3
 COMPAT_CFAR, COMPAT_MTI = 1, 2
+SPEC_F32, SPEC_F16 = 0, 1
 COMM_ID_BYTES = 128
 K_RANGE, K_DOPPLER, K_CFAR2D, K_COMPACT, K_FUSED, K_COUNT = 0, 1, 2, 3, 4, 5
 KERNEL_NAMES = ("k_range", "k_doppler", "k_cfar", "k_compact", "k_fused")
@@ -46,7 +47,7 @@ class FmcwConfig(C.Structure):
         ("cfar2d_scale_nom", C.c_uint32), ("cfar2d_scale_max", C.c_uint32),
         ("cfar2d_scale_override", C.c_uint32),
         ("max_frames", C.c_uint32), ("chunk_frames", C.c_uint32), ("device_id", C.c_int32),
-        ("compat_rtl", C.c_uint32), ("range_shift", C.c_uint32),
+        ("compat_rtl", C.c_uint32), ("range_shift", C.c_uint32), ("spectrum_dtype", C.c_int32),
     ]
 
 

@@ -139,7 +139,7 @@ class RadarCore:
                  cfar1d=(8, 2, 12, 4.0), in_dtype: str = "f32", window: str = "hamming",
                  magnitude: str = "abs", map_kind: str = "linear", max_frames: int = 1,
                  chunk_frames: int = 0, device: int = 0, mti_bypass: bool = True,
-                 NOTCH_MODE: int = 2, compat_rtl=(), range_shift: int = 0):
+                 NOTCH_MODE: int = 2, compat_rtl=(), range_shift: int = 0, spectrum: str = "f32"):
         """mti_bypass / NOTCH_MODE mirror radar_core's u_mti (radar_core.vhd:329-338, port
         :48).  The RTL port defaults to '0' (MTI on); this mirror defaults to bypass because
         the north-star path and BASELINE configs exclude MTI and tb_radar_core bypasses it
@@ -148,7 +148,9 @@ class RadarCore:
         compat_rtl: RTL-compat arithmetic (fmcw.h fmcw_compat): any of "cfar" (17-bit integer
         CFAR, os_cfar.vhd:132 / os_cfar_2d.vhd:189-199) and "mti" (int16 saturating canceller,
         doppler_notch.vhd:73-93).  range_shift: range spectrum scaled by 2^-range_shift (the
-        FFT IP's fixed scaling schedule), so that the MTI's 16-bit words are meaningful."""
+        FFT IP's fixed scaling schedule), so that the MTI's 16-bit words are meaningful.
+        spectrum: "f32" or "f16", the element type of the internal corner-turned spectrum
+        (fmcw.h fmcw_spectrum_dtype: "f16" halves its HBM traffic; map within 2e-3)."""
         lib = L.load()
         cfg = L.default_config()
         cfg.mti_mode = L.MTI_OFF if mti_bypass else {2: L.MTI_2PULSE, 3: L.MTI_3PULSE}[NOTCH_MODE]
@@ -170,6 +172,7 @@ class RadarCore:
         cfg.compat_rtl = compat_rtl if isinstance(compat_rtl, int) else \
             sum(flags[k] for k in set(compat_rtl))
         cfg.range_shift = range_shift
+        cfg.spectrum_dtype = {"f32": L.SPEC_F32, "f16": L.SPEC_F16}[spectrum]
         self.cfg = cfg
         self.in_dtype = in_dtype
         self.device = device

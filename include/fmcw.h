@@ -53,7 +53,8 @@
 extern "C" {
 #endif
 
-#define FMCW_ABI_VERSION 2  /* 2: fmcw_config grew compat_rtl, range_shift (27 words, 108 B) */
+#define FMCW_ABI_VERSION 3  /* 2: fmcw_config grew compat_rtl, range_shift (27 words, 108 B);
+                               3: + spectrum_dtype (28 words, 112 B) */
 
 typedef enum {
   FMCW_OK = 0,
@@ -119,7 +120,17 @@ typedef struct fmcw_config {
    * SCALE_SCH (tb_xfft_128.vhd:480-494), so that spectra fit the IP's 16-bit output word;
    * 0..13 */
   uint32_t range_shift;
+  /* fmcw_spectrum_dtype: element type of the internal corner-turned spectrum */
+  int32_t spectrum_dtype;
 } fmcw_config;
+
+/* fmcw_config.spectrum_dtype.  FMCW_SPEC_F16 stores the corner-turned spectrum (K1 -> K2) as
+ * fp16 pairs holding X / n_range: 4 instead of 8 bytes per point written and read back
+ * (config 5: 160 -> 128 MiB of HBM traffic per frame).  The map then carries fp16 rounding of
+ * the range spectrum: max |map - oracle| <= 2e-3 x max|oracle| per frame (tested), against
+ * 1e-4 for FMCW_SPEC_F32; detections stay bit-exact to the oracle CFAR on the map produced.
+ * Not with FMCW_COMPAT_MTI (its 16-bit words are defined on the fp32 spectrum). */
+typedef enum { FMCW_SPEC_F32 = 0, FMCW_SPEC_F16 = 1 } fmcw_spectrum_dtype;
 
 /* fmcw_config.compat_rtl bits.
  * FMCW_COMPAT_CFAR: the CFAR on the RTL's 17-bit unsigned cells (DATA_WIDTH 17): each map

@@ -43,7 +43,7 @@ def test_gfx950_code_object_present(lib_built):
 
 def test_struct_layouts():
     assert C.sizeof(L.FmcwDet) == 16
-    assert C.sizeof(L.FmcwConfig) == 27 * 4          # ABI 2 (fmcw.h FMCW_ABI_VERSION)
+    assert C.sizeof(L.FmcwConfig) == 28 * 4          # ABI 3 (fmcw.h FMCW_ABI_VERSION)
     assert L.FmcwDet.range.offset == 4 and L.FmcwDet.mag.offset == 8
 
 
@@ -57,8 +57,8 @@ def test_defaults_mirror_radar_core(lib_built):
             cfg.cfar2d_scale_max, cfg.cfar2d_scale_override) == (75, 2, 4, 6, 0)
     assert (cfg.cfar1d_ref, cfg.cfar1d_guard, cfg.cfar1d_rank) == (8, 2, 12)
     assert cfg.cfar1d_alpha == 4.0
-    assert lib_built.fmcw_abi_version() == 2
-    assert (cfg.compat_rtl, cfg.range_shift) == (0, 0)
+    assert lib_built.fmcw_abi_version() == 3
+    assert (cfg.compat_rtl, cfg.range_shift, cfg.spectrum_dtype) == (0, 0, L.SPEC_F32)
     assert b"gfx950" in lib_built.fmcw_version()
 
 
@@ -73,7 +73,7 @@ def test_defaults_mirror_radar_core(lib_built):
     ("cfar2d_rank_pct", 101, b"rank_pct"), ("cfar2d_rank_pct", 0xFFFFFFFF, b"rank_pct"),
     ("cfar2d_ref_range", 1 << 30, b"extents"),
     ("compat_rtl", 4, b"compat_rtl"), ("compat_rtl", 2, b"compat MTI"),   # MTI compat needs MTI on
-    ("range_shift", 14, b"range_shift"),
+    ("range_shift", 14, b"range_shift"), ("spectrum_dtype", 2, b"spectrum_dtype"),
 ])
 def test_create_rejects_bad_config(lib_built, field, value, msg):
     cfg = L.default_config()
@@ -83,6 +83,14 @@ def test_create_rejects_bad_config(lib_built, field, value, msg):
     assert rc == L.FMCW_EINVAL
     assert msg in lib_built.fmcw_last_error()
     assert not h.value
+
+
+def test_fp16_spectrum_excludes_compat_mti(lib_built):
+    cfg = L.default_config()
+    cfg.mti_mode, cfg.compat_rtl, cfg.spectrum_dtype = L.MTI_2PULSE, L.COMPAT_MTI, L.SPEC_F16
+    h = C.c_void_p()
+    assert lib_built.fmcw_create(C.byref(cfg), C.byref(h)) == L.FMCW_EINVAL
+    assert b"spectrum_dtype" in lib_built.fmcw_last_error()
 
 
 def test_compat_cfar_needs_integer_alpha(lib_built):

@@ -453,3 +453,43 @@ def test_cfar2d_strips_and_batched_launches(monkeypatch, steps):
     want = CB.cfar(out.rd_map, O.Cfar2D(), threads=16)
     np.testing.assert_array_equal(out.dets, want)
     assert out.n_dets > nf
+
+
+@pytest.mark.parametrize("ns,nc,nrx,dtype,cfar,mti", [
+    (8192, 1024, 1, "f16", "os2d", 0),   # BASELINE config 5 with the fp16 spectrum
+    (1024, 256, 1, "f32", "os1d", 0),    # config 2 geometry
+    (512, 64, 2, "i16", "os1d", 2),      # NCI over 2 rx, MTI 2-pulse on the fp16 spectrum
+    (256, 128, 1, "i16", "os2d", 3),
+])
+def test_fp16_spectrum(ns, nc, nrx, dtype, cfar, mti):
+    """FMCW_SPEC_F16 (fmcw.h): half2(X / N_range) between K1 and K2.  Map within the stated
+    2e-3 of the fp64 oracle per frame; CFAR bit-exact vs the C oracle on the map produced."""
+    nf = 1 if ns == 8192 else 2
+    cube = synth.frames(nf, ns, nc, nrx, "two_targets", dtype=dtype)
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, N_RX=nrx, in_dtype=dtype, cfar=cfar, max_frames=nf,
+                   mti_bypass=mti == 0, NOTCH_MODE=mti or 2, spectrum="f16") as core:
+        out = core.process(cube)
+    for f in range(nf):
+        ref = O.process(to_complex(cube[f], dtype), None, mti_mode=mti)["mag"]
+        assert rel_err(out.rd_map[f], ref) <= 2e-3
+    p = O.Cfar2D() if cfar == "os2d" else O.Cfar1D()
+    np.testing.assert_array_equal(out.dets, CB.cfar(out.rd_map, p, threads=16))
+    assert out.n_dets >= nf
+
+
+def test_fp16_spectrum_ambm_and_stage_api():
+    """AMBM on the fp16 spectrum against the fp32-spectrum path's map (2e-3), and
+    fmcw_range_ct still returning the fp32 spectrum (1e-4 vs the oracle) on an F16 handle."""
+    ns, nc, nf = 512, 64, 3
+    cube = synth.frames(nf, ns, nc, 1, "two_targets", dtype="i16")
+    maps = {}
+    for sp in ("f32", "f16"):
+        with RadarCore(N_RANGE=ns, N_DOPPLER=nc, in_dtype="i16", magnitude="ambm", cfar="os1d",
+                       max_frames=nf, spectrum=sp) as core:
+            maps[sp] = core.process(cube).rd_map
+            if sp == "f16":
+                spec = run_range_ct(core, cube, nf)
+    for f in range(nf):
+        assert rel_err(maps["f16"][f], maps["f32"][f]) <= 2e-3
+        ref = O.range_ct(to_complex(cube[f], "i16"))
+        assert rel_err(spec[f], ref) <= 1e-4
