@@ -23,6 +23,10 @@
 
 namespace fmcw {
 
+#ifndef FMCW_K1_HOLDW       // K1: range window held in registers: never (0), N >= 4096 (1), always (2)
+#define FMCW_K1_HOLDW 2
+#endif
+
 #ifndef FMCW_CFAR1D_WHOLE   // 1-D screen over the lane's whole window (1) or two 8-cell halves (0)
 #define FMCW_CFAR1D_WHOLE 1
 #endif
@@ -30,30 +34,44 @@ namespace fmcw {
 // --------------------------------------------------------------------------------------
 // Input loaders: two consecutive complex samples -> float4 (re0, im0, re1, im1).
 // ADC word {Q[31:16], I[15:0]} (rtl/src/tb_radar_core.vhd:115-118) = little-endian short2(I,Q).
+// fetch() issues the load and returns the raw bits; expand() converts them.  K1 prefetches the
+// raw bits and expands them only when it consumes them: a conversion next to the load would
+// make the prefetch wait for its data at once (fp16 / int16 input, config 5).
 // --------------------------------------------------------------------------------------
 struct LoadF32 {
   static constexpr int bytes = 8;
-  __device__ __forceinline__ static float4 load2(const void* base, size_t idx) {
+  using Raw = float4;
+  __device__ __forceinline__ static Raw fetch(const void* base, size_t idx) {
     return ld_f4<FMCW_NT_CUBE>(reinterpret_cast<const float2*>(base) + idx);
   }
+  __device__ __forceinline__ static float4 expand(Raw r) { return r; }
+  __device__ __forceinline__ static float4 load2(const void* base, size_t idx) { return fetch(base, idx); }
 };
 struct LoadF16 {
   static constexpr int bytes = 4;
-  __device__ __forceinline__ static float4 load2(const void* base, size_t idx) {
+  using Raw = fmcw_u2v;
+  __device__ __forceinline__ static Raw fetch(const void* base, size_t idx) {
+    return ld_u2<FMCW_NT_CUBE>(reinterpret_cast<const uint32_t*>(base) + idx);
+  }
+  __device__ __forceinline__ static float4 expand(Raw u) {
     typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-    const fmcw_u2v u = ld_u2<FMCW_NT_CUBE>(reinterpret_cast<const uint32_t*>(base) + idx);
     const h4 h = __builtin_bit_cast(h4, u);
     return make_float4((float)h[0], (float)h[1], (float)h[2], (float)h[3]);
   }
+  __device__ __forceinline__ static float4 load2(const void* base, size_t idx) { return expand(fetch(base, idx)); }
 };
 struct LoadI16 {
   static constexpr int bytes = 4;
-  __device__ __forceinline__ static float4 load2(const void* base, size_t idx) {
+  using Raw = fmcw_u2v;
+  __device__ __forceinline__ static Raw fetch(const void* base, size_t idx) {
+    return ld_u2<FMCW_NT_CUBE>(reinterpret_cast<const uint32_t*>(base) + idx);
+  }
+  __device__ __forceinline__ static float4 expand(Raw u) {
     typedef short s4 __attribute__((ext_vector_type(4)));
-    const fmcw_u2v u = ld_u2<FMCW_NT_CUBE>(reinterpret_cast<const uint32_t*>(base) + idx);
     const s4 s = __builtin_bit_cast(s4, u);
     return make_float4((float)s[0], (float)s[1], (float)s[2], (float)s[3]);
   }
+  __device__ __forceinline__ static float4 load2(const void* base, size_t idx) { return expand(fetch(base, idx)); }
 };
 
 // Corner-turned spectrum element: complex fp32 (8 B) or, with FMCW_SPEC_F16, a half2 (4 B)
@@ -124,12 +142,34 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
   const int rd0_off = c0 * REG + pad16(r0);
 
   int g = blockIdx.x;
-  float4 a[8];
+  typename LD::Raw a[8];  // this group's samples, raw (expanded at use)
+  // Doppler window of the next chirp, loaded with its samples: a vector load issued after the
+  // previous iteration's eight tile stores would make the wait for it (vmcnt counts in issue
+  // order) wait for those stores too.  From N = 1024 a wave holds one chirp (P >= 64), so the
+  // index is wave-uniform and the load goes through the scalar cache (lgkmcnt, not vmcnt).
+  auto cw_index = [](int i) { return P >= 64 ? __builtin_amdgcn_readfirstlane(i) : i; };
+  float cw_n = 1.f;
   if (g < n_groups) {
     const int fr = g / ncb;
-    const size_t chirp = (size_t)fr * nc + (size_t)(g - fr * ncb) * T + q;
+    const int cb = g - fr * ncb;
+    const size_t chirp = (size_t)fr * nc + (size_t)cb * T + q;
 #pragma unroll
-    for (int m = 0; m < 8; ++m) a[m] = LD::load2(cube, chirp * N + 2 * t0 + (N / 8) * m);
+    for (int m = 0; m < 8; ++m) a[m] = LD::fetch(cube, chirp * N + 2 * t0 + (N / 8) * m);
+    if (chirp_w) cw_n = chirp_w[cw_index(cb * T + q)];
+  }
+  // window coefficients for samples 2t + {0,1} + (N/8) m.  N >= 4096 (one or two workgroups
+  // per CU, so nothing else hides that store wait): held for the whole kernel.  Smaller N:
+  // re-read (L1/L2 hits) every group, 16 VGPRs fewer across the LDS passes (the register peak
+  // at 3 workgroups per CU).
+  constexpr bool HOLD_W = FMCW_K1_HOLDW >= 2 || (FMCW_K1_HOLDW == 1 && N >= 4096);
+  float2 wh[HOLD_W ? 8 : 1];
+  if constexpr (HOLD_W) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m) wh[m] = *reinterpret_cast<const float2*>(win + 2 * t0 + (N / 8) * m);
+    // complete them here: loads still in flight at the loop header make the compiler's
+    // wait there vmcnt(0), i.e. also on the previous iteration's tile stores
+#pragma unroll
+    for (int m = 0; m < 8; ++m) asm volatile("" ::"v"(wh[m].x), "v"(wh[m].y));
   }
   for (; g < n_groups; g += gridDim.x) {
     const int fr = g / ncb;  // frame*nrx + rx within this chunk
@@ -137,15 +177,17 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
     const int t = opaque(t0);
     float2* buf = lds + q * REG;
     // Doppler window of this chirp folded in (K2 then skips it; FFT linearity), or 1
-    const float cw = (chirp_w ? chirp_w[cb * T + q] : 1.f) * (H16 ? 1.0f / N : 1.0f);
+    const float cw = cw_n * (H16 ? 1.0f / N : 1.0f);
 
-    // window coefficients for samples 2t + {0,1} + (N/8) m, re-read (L1/L2 hits) every group
-    // rather than held: 16 VGPRs fewer across the LDS passes (the register peak)
     float2 w[8];
 #pragma unroll
-    for (int m = 0; m < 8; ++m) w[m] = *reinterpret_cast<const float2*>(win + 2 * t + (N / 8) * m);
+    for (int m = 0; m < 8; ++m)
+      w[m] = HOLD_W ? wh[HOLD_W ? m : 0] : *reinterpret_cast<const float2*>(win + 2 * t + (N / 8) * m);
 
     __syncthreads();  // previous group's transposed reads are done with lds
+    float4 ax[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) ax[m] = LD::expand(a[m]);
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       float2 v[8];
@@ -153,7 +195,7 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
       for (int m = 0; m < 8; ++m) {
         if constexpr (Q15) {
           const int c = (int)(e ? w[m].y : w[m].x);
-          const float xi = e ? a[m].z : a[m].x, xq = e ? a[m].w : a[m].y;
+          const float xi = e ? ax[m].z : ax[m].x, xq = e ? ax[m].w : ax[m].y;
           auto win16 = [c](float x) {
             const int y = ((int)x * c + (1 << 14)) >> 14;  // floor: arithmetic shift
             return (float)min(max(y, -32768), 32767);
@@ -162,7 +204,7 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
           v[m] = make_float2(win16(xi) * (cw * q15_scale), win16(xq) * (cw * q15_scale));
         } else {
           const float we = (e ? w[m].y : w[m].x) * cw;
-          v[m] = e ? make_float2(a[m].z * we, a[m].w * we) : make_float2(a[m].x * we, a[m].y * we);
+          v[m] = e ? make_float2(ax[m].z * we, ax[m].w * we) : make_float2(ax[m].x * we, ax[m].y * we);
         }
       }
       Dft<8>::run(v);
@@ -175,9 +217,11 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
       const int gn = g + gridDim.x;
       if (gn < n_groups) {
         const int frn = gn / ncb;
-        const size_t chirp = (size_t)frn * nc + (size_t)(gn - frn * ncb) * T + q;
+        const int cbn = gn - frn * ncb;
+        const size_t chirp = (size_t)frn * nc + (size_t)cbn * T + q;
 #pragma unroll
-        for (int m = 0; m < 8; ++m) a[m] = LD::load2(cube, chirp * N + 2 * t + (N / 8) * m);
+        for (int m = 0; m < 8; ++m) a[m] = LD::fetch(cube, chirp * N + 2 * t + (N / 8) * m);
+        if (chirp_w) cw_n = chirp_w[cw_index(cbn * T + q)];
       }
     }
     pass_sync<Gm::WG_SYNC>();
