@@ -634,6 +634,9 @@ __device__ __forceinline__ void cfar1d_wave(const float* mags, uint32_t* list, i
     // cells survive the screen on noise + targets, but they sit in ~8 of the 16 cell
     // indices, so counting per index for the whole wave (where any lane survived) cost 8 x 16
     // compares per lane; the ordered survivor list costs one 16-compare round per 64.
+#ifdef FMCW_CFAR1D_ABLATE  // timing experiments only: 2 = screen, no exact round
+    if (FMCW_CFAR1D_ABLATE == 2) bits = 0;
+#endif
     int n_surv;
     const int sx = wave_excl_scan(__popc(bits), n_surv);
     if (n_surv != 0) {  // uniform
@@ -1095,6 +1098,9 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
       }
     }
     if (cf.enabled)
+#ifdef FMCW_CFAR1D_ABLATE  // 1 = halos only, no CFAR
+      if (FMCW_CFAR1D_ABLATE != 1)
+#endif
       cfar1d_dispatch<NC>(mags, list, rr, t, r0, frame0 + f, tile0 + f * tiles_per_frame + lt, cf, sink);
     pass_sync<false>();  // the region is reused by the next tile
   }
