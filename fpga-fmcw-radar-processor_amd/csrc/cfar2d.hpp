@@ -263,6 +263,10 @@ __device__ __forceinline__ bool cfar2d_exact_a(const RowRing& rr, int rl, int d,
   if (a.n_ref - (int)nlt.x >= need) return false;                // E(s_min) >= need
   if (a.n_ref - (int)nlt.y < need || a.override_) return true;   // E(s2) may be < need
   const float half_up = sum * (1.0f + 1.0f / 32768.0f) / (float)a.n_ref * 0.5f;
+  // >= need refs lie above cut / s2; if cut / s2 >= mean / 2 they all lie above the half, so
+  // n_lo <= n_ref - need = rank < rank + 1 without counting (most noise survivors: their cut
+  // is high).  (1 - 2^-20) covers the product's rounding.
+  if (cut * (1.0f / s2) * (1.0f - 1.0f / 1048576.0f) >= half_up) return false;
   int n_lo = 0;
   visit([&](float v) { n_lo += v < half_up ? 1 : 0; });
   for (int x = 1; x < L; x <<= 1) n_lo += __shfl_xor(n_lo, x, 64);
