@@ -884,6 +884,9 @@ __device__ __forceinline__ int xcd_block_id(int bid, int grid) {
 #ifndef FMCW_K2_ORDER     // K2 tile order (see k_doppler)
 #define FMCW_K2_ORDER 1
 #endif
+#ifndef FMCW_K2_PF_NC     // K2: largest NC with the next-unit register prefetch
+#define FMCW_K2_PF_NC 256  // measured: no gain at NC = 512, 1024 (profiles/r02/k2_pf)
+#endif
 #ifndef FMCW_K2_WAVES     // K2 waves per SIMD asked of the register allocator (0 = by geometry)
 #define FMCW_K2_WAVES 0
 #endif
@@ -934,7 +937,7 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
   // registers right after this unit's first pass has consumed its own, so a wave keeps 8 KiB
   // of HBM reads in flight through its FFT, magnitude, map store and CFAR phases instead of
   // exposing the full load latency once per unit.
-  constexpr int NPF = MTI == 0 && NC <= 256 ? FMCW_K2_PREFETCH : 0;  // points loaded ahead
+  constexpr int NPF = MTI == 0 && NC <= FMCW_K2_PF_NC ? FMCW_K2_PREFETCH : 0;  // points loaded ahead
   constexpr bool PF = NPF > 0;
   // Tile order.  FMCW_K2_ORDER 0: frame-minor over all waves (tile -> f = tile % nf).
   // Measured on config 2: order 1 cuts K2 0.905 -> 0.874 us/frame (map-store cost 0.13 -> 0.085).
