@@ -493,3 +493,33 @@ def test_fp16_spectrum_ambm_and_stage_api():
         assert rel_err(maps["f16"][f], maps["f32"][f]) <= 2e-3
         ref = O.range_ct(to_complex(cube[f], "i16"))
         assert rel_err(spec[f], ref) <= 1e-4
+
+
+@pytest.mark.parametrize("ref_r,guard_r,ref_d,guard_d,pct,scales,steps", [
+    (4, 1, 4, 2, 75, (2, 4, 6), "2"),    # reference window: packed screen, strips of 2
+    (4, 1, 4, 2, 90, (3, 4, 5), "0"),    # screen with need = 13, other scales
+    (2, 1, 3, 1, 50, (1, 3, 5), "3"),    # other window: runtime-geometry phase A
+    (3, 0, 5, 3, 75, (2, 2, 2), "1"),    # no range guard, equal scales
+])
+def test_cfar2d_geometries_and_ranks(monkeypatch, ref_r, guard_r, ref_d, guard_d, pct, scales, steps):
+    """2-D CFAR at several windows, ranks and scale sets (oracle naming: ref/guard along range
+    and Doppler), Rayleigh clutter with targets and a quiet patch, 3 frames; bit-exact vs the
+    C oracle.  The pivoting k-th select runs at ranks other than 96 here."""
+    monkeypatch.setenv("FMCW_CFAR2D_STEPS", steps)
+    rng = np.random.default_rng(ref_r * 100 + pct)
+    m = rng.rayleigh(10.0, (3, 256, 128)).astype(np.float32)
+    m[:, 100:120, 20:40] = rng.rayleigh(150.0, (3, 20, 20))
+    m[:, 200:230, 60:90] = 0.02
+    m[0, 50, 7] = 900.0
+    m[1, 180, 127] = 700.0
+    m[2, 10:12, 64] = 800.0
+    p = O.Cfar2D(ref_range=ref_r, guard_range=guard_r, ref_doppler=ref_d, guard_doppler=guard_d,
+                 rank_pct=pct, scale_min=scales[0], scale_nom=scales[1], scale_max=scales[2])
+    with RadarCore(N_RANGE=256, N_DOPPLER=128, CFAR_REF_R=ref_d, CFAR_GUARD_R=guard_d, CFAR_REF_D=ref_r,
+                   CFAR_GUARD_D=guard_r, cfar_rank_pct=pct, cfar_scales=scales, cfar="os2d",
+                   max_frames=3) as core:
+        got, n, dropped = _stage_dets(core, m)
+    assert dropped == 0
+    want = CB.cfar(m, p, threads=16)
+    np.testing.assert_array_equal(got, want)
+    assert len(want) >= 3
