@@ -151,18 +151,28 @@ struct DopplerInfo {
   int WR, NT;  // range rows per wave tile, threads per workgroup (DopplerGeom::WPB tiles)
 };
 template <int N, bool H16>
-DopplerFn doppler_fn_t(int mti) {
+DopplerFn doppler_fn_t(int mti, bool fast) {
   return mti == FMCW_MTI_2PULSE   ? k_doppler<N, 2, H16>
          : mti == FMCW_MTI_3PULSE ? k_doppler<N, 3, H16>
+         : fast                   ? k_doppler<N, 0, H16, true>
                                   : k_doppler<N, 0, H16>;
 }
 template <int N>
-DopplerFn doppler_fn(int mti, bool h16) {
-  return h16 ? doppler_fn_t<N, true>(mti) : doppler_fn_t<N, false>(mti);
+DopplerFn doppler_fn(int mti, bool h16, bool fast) {
+  return h16 ? doppler_fn_t<N, true>(mti, fast) : doppler_fn_t<N, false>(mti, fast);
 }
-DopplerInfo doppler_info(uint32_t nc, int mti = FMCW_MTI_OFF, bool h16 = false) {
+// K2's FAST instantiation (kernels.hpp): MTI off, |X| magnitude, no dB map, and the 1-D CFAR
+// (if any) at the reference geometry in fp32
+bool k2_fast(const fmcw_config& c) {
+  const bool cfar_ok = c.cfar_kind != FMCW_CFAR_OS1D ||
+                       (c.cfar1d_ref == 8 && c.cfar1d_guard == 2 && (int)(2 * c.cfar1d_ref) - (int)c.cfar1d_rank <= 4 &&
+                        !(c.compat_rtl & FMCW_COMPAT_CFAR));
+  return c.mti_mode == FMCW_MTI_OFF && c.mag_mode != FMCW_MAG_AMBM && c.map_kind != FMCW_MAP_DB && cfar_ok &&
+         !std::getenv("FMCW_K2_GENERIC");
+}
+DopplerInfo doppler_info(uint32_t nc, int mti = FMCW_MTI_OFF, bool h16 = false, bool fast = false) {
   switch (nc) {
-#define D_(N) case N: return {doppler_fn<N>(mti, h16), DopplerGeom<N>::WR, DopplerGeom<N>::NT};
+#define D_(N) case N: return {doppler_fn<N>(mti, h16, fast), DopplerGeom<N>::WR, DopplerGeom<N>::NT};
     D_(32) D_(64) D_(128) D_(256) D_(512) D_(1024)
 #undef D_
   }
@@ -752,7 +762,7 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
 #ifdef FMCW_K1_GRID_PER_CU  // tuning switch (tools/build_variants.sh): K1 workgroups per CU
   h->grid_range = std::min(h->grid_range, FMCW_K1_GRID_PER_CU * h->n_cu);
 #endif
-  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype == FMCW_SPEC_F16);
+  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype == FMCW_SPEC_F16, k2_fast(c));
   occupancy_grid(di.fn, di.NT, 0, h->n_cu, &h->grid_doppler);
   if (c.cfar_kind == FMCW_CFAR_OS2D) {
     const Cfar2DArgs a = cfar2_args(c);
@@ -808,7 +818,7 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
   HIP_TRY(hipSetDevice(c.device_id));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, c.spectrum_dtype == FMCW_SPEC_F16);
-  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype == FMCW_SPEC_F16);
+  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype == FMCW_SPEC_F16, k2_fast(c));
   const size_t frame_px = (size_t)c.n_range * c.n_doppler;
   const size_t in_frame_bytes = cube_bytes(c, 1);
   const Cfar1DArgs cf1 = cfar1_args(c);

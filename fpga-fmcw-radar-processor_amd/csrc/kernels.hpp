@@ -444,16 +444,24 @@ template <int NC> struct DopplerGeom {
   static_assert(WFL % 4 == 0 && REGM % 4 == 0, "16-B aligned rows and regions");
 };
 
-// Wave-level exclusive scan (shuffles only); `total` = the wave's sum, uniform.
+// Wave-level exclusive scan; `total` = the wave's sum, uniform.  DPP adds on the VALU (GCN
+// row scan: row_shr 1/2/4/8 inside each row of 16 lanes, then row_bcast:15 / row_bcast:31 carry
+// the row totals), where the former __shfl_up version took six ds_bpermute round trips through
+// LDS plus a lane-mask select per step (SGPR pressure).  Every caller runs it with the whole wave
+// active.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ int dpp_add(int x) {
+  return x + __builtin_amdgcn_update_dpp(0, x, CTRL, ROW_MASK, 0xf, false);
+}
 __device__ __forceinline__ int wave_excl_scan(int v, int& total) {
-  const int lane = threadIdx.x & 63;
   int x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
-  total = __shfl(x, 63, 64);
+  x = dpp_add<0x111, 0xf>(x);  // row_shr:1
+  x = dpp_add<0x112, 0xf>(x);  // row_shr:2
+  x = dpp_add<0x114, 0xf>(x);  // row_shr:4
+  x = dpp_add<0x118, 0xf>(x);  // row_shr:8
+  x = dpp_add<0x142, 0xa>(x);  // row_bcast:15 -> rows 1, 3
+  x = dpp_add<0x143, 0xc>(x);  // row_bcast:31 -> rows 2, 3
+  total = __builtin_amdgcn_readlane(x, 63);
   return x - v;
 }
 
@@ -479,11 +487,16 @@ __device__ __forceinline__ uint32_t det_reserve_wave(const DetSink& sink, int ti
 
 // exact k-th smallest of 2*REF registers: bitonic sort (compile-time indices), then the max of
 // the ascending prefix r[0..rank] (a select chain `i == rank ? r[i] : out` is turned by LLVM
-// into a private-array lookup, i.e. a scratch store + indexed load per detection)
+// into a private-array lookup, i.e. a scratch store + indexed load per detection).  On the bit
+// patterns: CFAR cells are non-negative (unsigned order == value order), and integer min/max need
+// none of the NaN-canonicalising v_max_f32 x, x, x that fminf/fmaxf of loaded values cost.
 template <int REF, int GUARD>
-__device__ __forceinline__ float ranked_of(float (&r)[2 * REF], int rank) {
+__device__ __forceinline__ float ranked_of(float (&rf)[2 * REF], int rank) {
   constexpr int N = 2 * REF;
   static_assert((N & (N - 1)) == 0, "power-of-two reference count");
+  uint32_t r[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = __float_as_uint(rf[i]);
 #pragma unroll
   for (int k = 2; k <= N; k <<= 1)
 #pragma unroll
@@ -492,16 +505,16 @@ __device__ __forceinline__ float ranked_of(float (&r)[2 * REF], int rank) {
       for (int i = 0; i < N; ++i) {
         const int l = i ^ j;
         if (l > i) {
-          const float a = r[i], b = r[l];
+          const uint32_t a = r[i], b = r[l];
           const bool up = (i & k) == 0;
-          r[i] = up ? fminf(a, b) : fmaxf(a, b);
-          r[l] = up ? fmaxf(a, b) : fminf(a, b);
+          r[i] = up ? min(a, b) : max(a, b);
+          r[l] = up ? max(a, b) : min(a, b);
         }
       }
-  float out = r[0];
+  uint32_t out = r[0];
 #pragma unroll
-  for (int i = 1; i < N; ++i) out = fmaxf(out, i <= rank ? r[i] : r[0]);
-  return out;
+  for (int i = 1; i < N; ++i) out = max(out, i <= rank ? r[i] : r[0]);
+  return __uint_as_float(out);
 }
 
 // 1-D OS-CFAR along Doppler (circular) over a wave tile's magnitude rows, plus ordered
@@ -512,7 +525,10 @@ __device__ __forceinline__ float ranked_of(float (&r)[2 * REF], int rank) {
 // integer arithmetic (lt_bit) so that hundreds of compares do not become SGPR masks.
 // REF > 0: compile-time geometry (REF refs + GUARD guards per side) with the window in
 // registers, screened (below); REF == 0: runtime geometry read from LDS.
-template <int NC, int REF, int GUARD>
+// ONEG: need = n_ref - rank <= 4 known at compile time (the reference's rank 12 of 16), so
+// one qualifying group of 4 rejects and the per-cell screen is a 4-way max (no runtime branch
+// per cell, which also kept both screens' registers live).
+template <int NC, int REF, int GUARD, bool ONEG = false>
 __device__ __forceinline__ void cfar1d_wave(const float* mags, uint32_t* list, int rr, int t, int r0,
                                             int frame, int tile, const Cfar1DArgs& cf,
                                             const DetSink& sink) {
@@ -539,7 +555,7 @@ __device__ __forceinline__ void cfar1d_wave(const float* mags, uint32_t* list, i
     // two halves of 8 cells (a 28-value window each) to keep the register peak low
     const float* lb = mrow + midx(d0);
     const int need = nref - cf.rank;
-    const bool one_group = need <= 4;          // the reference (rank 12 of 16): any group rejects
+    constexpr bool one_group = ONEG;           // the reference (rank 12 of 16): any group rejects
 #if FMCW_CFAR1D_WHOLE
     // The lane's whole window at once: cells d0 - H .. d0 + 15 + H, group minima g[k] =
     // min(w[k .. k+3]) over it computed once (2 mins per group), not per 8-cell half.
@@ -547,38 +563,43 @@ __device__ __forceinline__ void cfar1d_wave(const float* mags, uint32_t* list, i
       constexpr int WW = CELLS + 2 * H;        // 36 at the reference geometry
       constexpr int O0 = floor4(-H);
       constexpr int NV = (WW + (-H - O0) + 3) / 4;
-      float v[4 * NV];
-      load_cells<NV>(lb, O0, v);
-      float g[WW - 3];
+      float vf[4 * NV];
+      load_cells<NV>(lb, O0, vf);
+      // group minima and maxima on the bit patterns (non-negative cells: unsigned order is the
+      // float order; v_min/max_u32 need no NaN canonicalisation, v_min3/max3_u32 fold pairs)
+      uint32_t v[4 * NV];
+#pragma unroll
+      for (int k = 0; k < 4 * NV; ++k) v[k] = __float_as_uint(vf[k]);
+      uint32_t g[WW - 3];
       {
-        float m2[WW - 1];
+        uint32_t m2[WW - 1];
 #pragma unroll
-        for (int k = 0; k < WW - 1; ++k) m2[k] = fminf(v[-H - O0 + k], v[-H - O0 + k + 1]);
+        for (int k = 0; k < WW - 1; ++k) m2[k] = min(v[-H - O0 + k], v[-H - O0 + k + 1]);
 #pragma unroll
-        for (int k = 0; k < WW - 3; ++k) g[k] = fminf(m2[k], m2[k + 2]);
+        for (int k = 0; k < WW - 3; ++k) g[k] = min(m2[k], m2[k + 2]);
       }
 #pragma unroll
       for (int i = 0; i < CELLS; ++i) {
-        const float cut = v[-O0 + i];
+        const float cut = vf[-O0 + i];
         uint32_t sb;
         if (one_group) {
           // reject <=> alpha M >= cut for the largest group minimum M.  fma(alpha, M, -cut) < 0
           // (exact product) survives a few cells the rounded test would reject -- never the
           // reverse (alpha M >= cut exactly implies fl(alpha M) >= cut) -- and the exact count
           // below decides those, so the screen stays conservative.  Sign bit = survival.
-          float M = g[i];
+          uint32_t M = g[i];
 #pragma unroll
-          for (int q = 1; q < NGS; ++q) M = fmaxf(M, g[i + 4 * q]);
+          for (int q = 1; q < NGS; ++q) M = max(M, g[i + 4 * q]);
 #pragma unroll
-          for (int q = 0; q < NGS; ++q) M = fmaxf(M, g[i + RO + 4 * q]);
-          sb = __float_as_uint(__builtin_fmaf(cf.alpha, M, -cut)) >> 31;
+          for (int q = 0; q < NGS; ++q) M = max(M, g[i + RO + 4 * q]);
+          sb = __float_as_uint(__builtin_fmaf(cf.alpha, __uint_as_float(M), -cut)) >> 31;
         } else {
           const uint32_t cbits = __float_as_uint(cut);
           uint32_t nlt = 0;  // groups with alpha * min < cut
 #pragma unroll
           for (int q = 0; q < NGS; ++q)
-            nlt += lt_bit(__float_as_uint(cf.alpha * g[i + 4 * q]), cbits) +
-                   lt_bit(__float_as_uint(cf.alpha * g[i + RO + 4 * q]), cbits);
+            nlt += lt_bit(__float_as_uint(cf.alpha * __uint_as_float(g[i + 4 * q])), cbits) +
+                   lt_bit(__float_as_uint(cf.alpha * __uint_as_float(g[i + RO + 4 * q])), cbits);
           sb = 4 * (2 * NGS - (int)nlt) < need ? 1u : 0u;
         }
         bits |= sb << i;
@@ -808,6 +829,8 @@ __device__ __forceinline__ void cfar1d_dispatch(const float* mags, uint32_t* lis
                                                 const DetSink& sink) {
   if (cf.compat)
     cfar1d_wave_rtl<NC>(mags, list, rr, t, r0, frame, tile, cf, sink);
+  else if (cf.ref == 8 && cf.guard == 2 && 2 * cf.ref - cf.rank <= 4)
+    cfar1d_wave<NC, 8, 2, true>(mags, list, rr, t, r0, frame, tile, cf, sink);
   else if (cf.ref == 8 && cf.guard == 2)
     cfar1d_wave<NC, 8, 2>(mags, list, rr, t, r0, frame, tile, cf, sink);
   else
@@ -894,7 +917,11 @@ template <int NC, int MTI>
 constexpr int k2_waves() {
   return FMCW_K2_WAVES > 0 ? FMCW_K2_WAVES : (MTI == 0 && NC <= 256 && FMCW_K2_PREFETCH <= 8) ? 3 : 2;
 }
-template <int NC, int MTI, bool H16 = false>
+// FAST: the common configuration fixed at compile time -- |X| magnitude (no AMBM), no dB map,
+// and the 1-D CFAR, when enabled, at the reference geometry (8 refs / 2 guards per side, need =
+// n_ref - rank <= 4, fp32 compare).  The generic kernel keeps those as uniform runtime branches,
+// whose other arms held registers and SGPRs (spills to VGPR lanes) across the tile loop.
+template <int NC, int MTI, bool H16 = false, bool FAST = false>
 __global__ void __launch_bounds__(DopplerGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(k2_waves<NC, MTI>())))
 k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, int ns, int nrx,
           int lgT, int lgRB, int n_tiles, int frame0, int tile0, float* __restrict__ lin_map,
@@ -1048,7 +1075,7 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
       float2 X[LG][LR];
       if constexpr (TWH) stockham_last_tw<NC, 16, P>(buf, t, X, twh);
       else stockham_to_regs<NC, 16, P, false>(buf, t, X);
-      if (mag_mode == FMCW_MAG_AMBM) {  // uniform: one branch for the whole block
+      if (!FAST && mag_mode == FMCW_MAG_AMBM) {  // uniform: one branch for the whole block
 #pragma unroll
         for (int g = 0; g < LG; ++g)
 #pragma unroll
@@ -1066,7 +1093,7 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
       pass_sync<false>();  // every read of the last pass is issued: the rows may be rewritten
     }
     // magnitudes -> the wave region (over the dead FFT rows), for the map store and the CFAR
-    const bool ambm = mag_mode == FMCW_MAG_AMBM;
+    const bool ambm = !FAST && mag_mode == FMCW_MAG_AMBM;
     float* mrow = mags + rr * REGM;
 #pragma unroll
     for (int g = 0; g < LG; ++g) {
@@ -1092,7 +1119,7 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
         const int rl = e / NC, d = e - rl * NC;
         const float4 v = *reinterpret_cast<const float4*>(mags + rl * REGM + midx(d));
         if (lin_map) st_f4<FMCW_NT_MAP>(lin_map + mbase + e, v);
-        if (db_map) {
+        if (!FAST && db_map) {
           const float k = 6.0205999132796239f;  // 20 / log2(10)
           *reinterpret_cast<float4*>(db_map + mbase + e) =
               make_float4(k * __log2f(v.x + 1.f), k * __log2f(v.y + 1.f), k * __log2f(v.z + 1.f),
@@ -1104,7 +1131,12 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
 #ifdef FMCW_CFAR1D_ABLATE  // 1 = halos only, no CFAR
       if (FMCW_CFAR1D_ABLATE != 1)
 #endif
-      cfar1d_dispatch<NC>(mags, list, rr, t, r0, frame0 + f, tile0 + f * tiles_per_frame + lt, cf, sink);
+    {
+      if constexpr (FAST)
+        cfar1d_wave<NC, 8, 2, true>(mags, list, rr, t, r0, frame0 + f, tile0 + f * tiles_per_frame + lt, cf, sink);
+      else
+        cfar1d_dispatch<NC>(mags, list, rr, t, r0, frame0 + f, tile0 + f * tiles_per_frame + lt, cf, sink);
+    }
     pass_sync<false>();  // the region is reused by the next tile
   }
 }

@@ -43,6 +43,12 @@ for s in "$@"; do
     gpu_cfar_tests) run pytest_cfar 600 python -u -m pytest tests -m gpu -v -x -k "cfar or 2d or os2d or config5 or c5 or tb" --timeout 170 --timeout-method thread -p no:cacheprovider ;;
     pmcf_c*) w=${s#pmcf_}; run "pmcf_$w" 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmcf_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
     pmcw_c*) w=${s#pmcw_}; run "pmcw_$w" 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcw_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
+    bench_generic) FMCW_K2_GENERIC=1 run bench_generic 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
+    bench_quick) run bench_quick 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
+    chunk_sweep)  # config-2 bench per K1/K2 chunk size (frames per launch)
+      for c in ${CHUNKS:-96 128 256 512 1024}; do
+        run "bench_chunk$c" 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d --chunk "$c"
+      done ;;
     counters) run counters 120 rocprofv3 -L ;;
     prof_c*) w=${s#prof_}; run "rocprof_stats_$w" 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 5 --warmup 2 --no-cpu-baseline --no-h2d ;;
     pmcsq_c*) w=${s#pmcsq_}; run "pmcsq_$w" 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/pmcsq_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
