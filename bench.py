@@ -219,6 +219,10 @@ def main():
     if ms_d:
         kern["k_doppler"]["GBps_algorithmic"] = bytes_dopp / (ms_d * 1e-3) / 1e9
     ms_f, n_f = kt["k_fused"]
+    ms_p, n_p = kt["k_pair"]
+    if ms_p:
+        # paired launches (pair.hpp): K1's and K2's algorithmic bytes move in the same launches
+        kern["k_pair"]["GBps_algorithmic"] = (bytes_range + bytes_dopp) / (ms_p * 1e-3) / 1e9
     pmc = {}
     pmc_file = REPO / "profiles" / PMC_FILE
     if pmc_file.exists():
@@ -239,6 +243,18 @@ def main():
                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                     "bytes_per_launch": bytes_fused // max(1, n_f),
                     "avg_launch_ms": round(ms_f / n_f, 5)}
+    elif n_p:
+        # range + Doppler stages in one launch: cube in + spectrum out + spectrum in + map out
+        achieved = (bytes_range + bytes_dopp) / (ms_p * 1e-3) / 1e9
+        traffic = None
+        if pmc.get("workload") == args.workload and pmc.get("frames_per_launch") == F // max(1, n_p // args.steps):
+            traffic = pmc.get("k_pair_bytes_per_launch")
+        roofline = {"kernel": "k_pair (range stage of chunk c beside the Doppler stage + |X| + map + 1-D CFAR "
+                              "of chunk c-1)", "bound": "hbm",
+                    "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                    "bytes_per_launch": (bytes_range + bytes_dopp) // max(1, n_p),
+                    "avg_launch_ms": round(ms_p / n_p, 5)}
     else:
         achieved = bytes_range / (ms_r * 1e-3) / 1e9 if ms_r else None
         traffic = None
@@ -349,6 +365,8 @@ def main():
         "e2e_GBps_algorithmic": round(e2e_bytes * args.steps * world / elapsed / 1e9, 1),
         "e2e_frac_of_peak": round(e2e_bytes * args.steps / elapsed / 1e9 / HBM_PEAK_GBPS, 4),
         "fused_path": bool(core.info("fused")),
+        "chunk_frames": core.info("chunk"),
+        "pair_chunk_frames": core.info("pair_chunk"),
         "detections_per_step": n_det_step,
         "roofline": roofline,
         "kernels": kern,

@@ -102,6 +102,11 @@ struct fmcw_handle {
   uint64_t* fused_trace = nullptr;  // FMCW_FUSED_TRACE=1: phase timestamps of every launch
   int64_t fused_fallbacks = 0;
   bool fused_used_last = false;  // the last fmcw_enqueue ran the fused kernel
+  // paired K1 + K2 launches (pair.hpp): chunk c's range stage beside chunk c - 1's Doppler stage
+  void (*pair_fn)(PairArgs) = nullptr;
+  uint32_t pair_chunk = 0;       // frames per chunk; two chunk spectra (h->inter, pair_b) in flight
+  float2* pair_b = nullptr;
+  int grid_pair = 0;
   // profiling
   bool profiling = false;
   std::vector<PendingEvent> pending;
@@ -231,6 +236,17 @@ FusedInfo fused_info(uint32_t n, uint32_t nc, int dtype) {
   F_(1024, 256) F_(1024, 128) F_(512, 256) F_(2048, 128)
 #undef F_
   return {nullptr, 0, 0};
+}
+
+// paired K1 + K2 instantiations: BASELINE config 2 (1024 x 256)
+using PairFn = void (*)(PairArgs);
+PairFn pair_fn(uint32_t n, uint32_t nc, int dtype) {
+  if (n == 1024 && nc == 256) switch (dtype) {
+      case FMCW_IN_F32: return k_pair<1024, 256, LoadF32>;
+      case FMCW_IN_F16: return k_pair<1024, 256, LoadF16>;
+      case FMCW_IN_I16: return k_pair<1024, 256, LoadI16>;
+    }
+  return nullptr;
 }
 
 // 2-D CFAR derived parameters
@@ -604,6 +620,34 @@ void setup_fused(fmcw_handle* h) {
   h->fused_ok = true;
 }
 
+// Paired launches (pair.hpp), default on where instantiated: one rx, MTI off, the FAST K2
+// configuration without the 2-D CFAR, fp32 window and spectrum.  Chunk: the largest multiple of
+// the frames one round of the persistent grid covers with both chunk spectra (written and read)
+// within ~3/4 of the 256 MiB Infinity Cache.  FMCW_PAIR=0 / 1 overrides kPairDefault (A/B runs).
+constexpr bool kPairDefault = false;
+void setup_pair(fmcw_handle* h, size_t frame_inter) {
+  const fmcw_config& c = h->cfg;
+  const char* env = std::getenv("FMCW_PAIR");
+  if (!(env ? env[0] == '1' : kPairDefault)) return;
+  if (c.n_rx != 1 || c.window == FMCW_WIN_Q15_RTL || c.spectrum_dtype != FMCW_SPEC_F32 ||
+      c.cfar_kind == FMCW_CFAR_OS2D || !k2_fast(c))
+    return;
+  const PairFn fn = pair_fn(c.n_range, c.n_doppler, c.in_dtype);
+  if (!fn) return;
+  occupancy_grid(fn, 256, 0, h->n_cu, &h->grid_pair);
+  const size_t tpf = (size_t)c.n_range / doppler_info(c.n_doppler).WR;
+  const size_t units_pf = tpf / kWavesPerBlock;  // K2 items per frame (K1: n_doppler / T)
+  size_t ch = std::max<size_t>(1, (192u << 20) / (2 * frame_inter));
+  if ((size_t)h->grid_pair % units_pf == 0) {
+    const size_t unit = (size_t)h->grid_pair / units_pf;
+    if (ch >= 2 * unit) ch -= ch % unit;
+  }
+  if (const char* pc = std::getenv("FMCW_PAIR_CHUNK")) ch = (size_t)std::max(1, std::atoi(pc));
+  h->pair_chunk = (uint32_t)std::min<size_t>(ch, c.max_frames);
+  if (h->pair_chunk >= c.max_frames) return;  // a batch never spans two chunks: nothing to pair
+  h->pair_fn = fn;
+}
+
 // the thread-local fmcw_last_error() message, for the other translation units of the library
 int fmcw_internal_fail(int code, const char* msg) { return fail(code, "%s", msg); }
 
@@ -643,6 +687,26 @@ void fmcw_config_default(fmcw_config* c) {
   c->device_id = 0;
 }
 
+// Frames per K1 -> K2 chunk when the caller leaves chunk_frames at 0.  The corner-turned
+// spectrum of a chunk is written by K1 and read back by K2 right after; kept to ~3/4 of the
+// 256 MiB Infinity Cache (MALL), K2's reads hit there.  Measured on config 2 (round 2, 1024
+// frames per step, gpurun_out chunk sweep): K2 0.63 us/frame at 128 frames (256 MiB), 0.57 at
+// 96, 0.55 at 108-120, 0.81 from 256 frames up (reads from HBM); K1 unchanged.  Within that,
+// a multiple of the frames one full round of K2's persistent grid covers (config 2: 3072
+// waves / 256 wave tiles = 12 frames, K1 the same), so neither kernel ends on a partial round.
+uint32_t auto_chunk(const fmcw_handle* h, size_t frame_inter) {
+  const fmcw_config& c = h->cfg;
+  constexpr size_t kMallBudget = 192u << 20;
+  size_t ch = std::max<size_t>(1, kMallBudget / frame_inter);
+  const size_t waves = (size_t)h->grid_doppler * kWavesPerBlock;
+  const size_t tpf = (size_t)c.n_range / doppler_info(c.n_doppler).WR;
+  if (waves % tpf == 0) {
+    const size_t unit = waves / tpf;  // frames per full K2 round
+    if (ch >= 2 * unit) ch -= ch % unit;
+  }
+  return (uint32_t)std::min<size_t>(c.max_frames, ch);
+}
+
 int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   if (!cfg || !out) return fail(FMCW_EINVAL, "null argument");
   *out = nullptr;
@@ -672,6 +736,12 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   h->lgRB = __builtin_ctz(ri.RB);
   const size_t frame_inter = (size_t)c.n_rx * c.n_range * c.n_doppler *
                              (c.spectrum_dtype == FMCW_SPEC_F16 ? sizeof(uint32_t) : sizeof(float2));
+  occupancy_grid(ri.fn, ri.NT, 0, h->n_cu, &h->grid_range);
+#ifdef FMCW_K1_GRID_PER_CU  // tuning switch (tools/build_variants.sh): K1 workgroups per CU
+  h->grid_range = std::min(h->grid_range, FMCW_K1_GRID_PER_CU * h->n_cu);
+#endif
+  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype == FMCW_SPEC_F16, k2_fast(c));
+  occupancy_grid(di.fn, di.NT, 0, h->n_cu, &h->grid_doppler);
   // two-stream pipeline of chunks (FMCW_PIPE=1): ring of FMCW_PIPE_BUFS intermediate buffers of
   // FMCW_PIPE_CHUNK frames, sized so the ring stays in the 256 MiB Infinity Cache
   if (const char* cs = std::getenv("FMCW_CFAR2D_STEPS")) h->cfar2_steps = std::max(0, std::atoi(cs));
@@ -686,10 +756,7 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   } else if (c.chunk_frames) {
     h->chunk = std::min<uint32_t>(c.chunk_frames, c.max_frames);
   } else {
-    // ~256 MiB of corner-turned intermediate per chunk: measured on config 2, 32 -> 128 frames
-    // per launch cuts K1 0.90 -> 0.72 us/frame and K2 by ~5 % (fewer launch tails; the
-    // MALL-resident 64 MiB chunk saved less than the extra launches cost)
-    h->chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(c.max_frames, (256u << 20) / frame_inter));
+    h->chunk = auto_chunk(h, frame_inter);
   }
   auto cleanup = [&](int code) {
     fmcw_destroy(h);
@@ -705,8 +772,11 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   ALLOC(h->win_r, c.n_range * sizeof(float));
   ALLOC(h->win_d, c.n_doppler * sizeof(float));
   // >= one fp32 frame: fmcw_range_ct writes the fp32 spectrum through it whatever spectrum_dtype
-  h->inter_bytes = std::max(h->chunk * frame_inter, (size_t)c.n_rx * c.n_range * c.n_doppler * sizeof(float2));
+  setup_pair(h, frame_inter);
+  h->inter_bytes = std::max(std::max<size_t>(h->chunk, h->pair_fn ? h->pair_chunk : 0) * frame_inter,
+                            (size_t)c.n_rx * c.n_range * c.n_doppler * sizeof(float2));
   ALLOC(h->inter, h->inter_bytes);
+  if (h->pair_fn) ALLOC(h->pair_b, (size_t)h->pair_chunk * frame_inter);
   if (c.cfar_kind == FMCW_CFAR_OS2D) ALLOC(h->lin_scratch, (size_t)h->chunk * c.n_range * c.n_doppler * sizeof(float));
   if (h->pipe_nb) {
     h->inter_b[0] = h->inter;
@@ -758,12 +828,6 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
         hipMemset(h->wg_count, 0, h->n_wg_max * sizeof(uint32_t)) != hipSuccess)
       return cleanup(fail(FMCW_EHIP, "window upload failed"));
   }
-  occupancy_grid(ri.fn, ri.NT, 0, h->n_cu, &h->grid_range);
-#ifdef FMCW_K1_GRID_PER_CU  // tuning switch (tools/build_variants.sh): K1 workgroups per CU
-  h->grid_range = std::min(h->grid_range, FMCW_K1_GRID_PER_CU * h->n_cu);
-#endif
-  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype == FMCW_SPEC_F16, k2_fast(c));
-  occupancy_grid(di.fn, di.NT, 0, h->n_cu, &h->grid_doppler);
   if (c.cfar_kind == FMCW_CFAR_OS2D) {
     const Cfar2DArgs a = cfar2_args(c);
     h->cfar2d_smem = cfar2_smem(c.n_doppler, a.hr);
@@ -783,7 +847,8 @@ int fmcw_destroy(fmcw_handle* h) {
   hipSetDevice(h->cfg.device_id);
   void* ptrs[] = {h->win_r, h->win_d, h->inter, h->lin_scratch, h->det_scratch, h->counter,
                   h->n_dets_tmp, h->wg_base, h->wg_count, h->wg_off, h->block_sum,
-                  h->stage_cube, h->stage_map, h->stage_dets, h->fused_spec, h->fused_ctl, h->fused_trace};
+                  h->stage_cube, h->stage_map, h->stage_dets, h->fused_spec, h->fused_ctl, h->fused_trace,
+                  h->pair_b};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& pe : h->pending) {
@@ -863,6 +928,42 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
         const int nf = (int)std::min<size_t>(std::max<size_t>(h->chunk, kCfar2Batch), n_frames - f0);
         if ((rc = launch_cfar(h, rd_map + f0 * frame_px, nf, (int)f0, s))) return rc;
       }
+    if (c.cfar_kind != FMCW_CFAR_NONE) return launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, s);
+    return FMCW_OK;
+  }
+
+  // Paired launches: launch i runs K1 of chunk i into buffer i % 2 beside K2 of chunk i - 1
+  // from buffer (i - 1) % 2; the kernel boundary orders every write before its read
+  if (h->pair_fn && n_frames > h->pair_chunk) {
+    const size_t C = h->pair_chunk;
+    const size_t n_chunks = (n_frames + C - 1) / C;
+    const size_t tpf = c.n_range / di.WR;
+    float2* bufs[2] = {h->inter, h->pair_b};
+    for (size_t i = 0; i <= n_chunks; ++i) {
+      PairArgs a{};
+      a.win_r = h->win_r;
+      a.chirp_w = h->win_d;
+      a.cf = cf1;
+      a.sink = sink;
+      if (i < n_chunks) {
+        const size_t f0 = i * C, nf = std::min(C, n_frames - f0);
+        a.cube = static_cast<const char*>(cube) + f0 * in_frame_bytes;
+        a.inter_w = bufs[i & 1];
+        a.n_groups = (int)(nf * (c.n_doppler / ri.T));
+      }
+      if (i >= 1) {
+        const size_t f0 = (i - 1) * C, nf = std::min(C, n_frames - f0);
+        a.inter_r = bufs[(i - 1) & 1];
+        a.n_tiles = (int)(nf * tpf);
+        a.frame0 = (int)f0;
+        a.tile0 = (int)(f0 * tpf);
+        a.lin_map = rd_map && c.map_kind == FMCW_MAP_LINEAR ? rd_map + f0 * frame_px : nullptr;
+      }
+      const int items = std::max(a.n_groups, a.n_tiles / kWavesPerBlock);
+      ProfScope ps(h, FMCW_K_PAIR, s);
+      hipLaunchKernelGGL(h->pair_fn, dim3(std::min(items, h->grid_pair)), dim3(256), 0, s, a);
+      if ((rc = check_launch("k_pair"))) return rc;
+    }
     if (c.cfar_kind != FMCW_CFAR_NONE) return launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, s);
     return FMCW_OK;
   }
@@ -1068,6 +1169,7 @@ int fmcw_get_info(fmcw_handle* h, int key, int64_t* value) {
     case FMCW_INFO_FUSED_GROUP: *value = h->fused_per_xcd; return FMCW_OK;
     case FMCW_INFO_FUSED_FALLBACKS: *value = h->fused_fallbacks; return FMCW_OK;
     case FMCW_INFO_CHUNK: *value = h->chunk; return FMCW_OK;
+    case FMCW_INFO_PAIR_CHUNK: *value = h->pair_fn ? h->pair_chunk : 0; return FMCW_OK;
   }
   return fail(FMCW_EINVAL, "fmcw_get_info: unknown key %d", key);
 }

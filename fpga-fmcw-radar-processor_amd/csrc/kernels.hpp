@@ -1151,6 +1151,11 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
 // --------------------------------------------------------------------------------------
 #include "fused.hpp"
 
+// --------------------------------------------------------------------------------------
+// K12p: K1 of chunk c beside K2 of chunk c - 1 in one launch (double-buffered) -- see pair.hpp.
+// --------------------------------------------------------------------------------------
+#include "pair.hpp"
+
 
 // --------------------------------------------------------------------------------------
 // Detection ordering: exclusive scan over per-workgroup counts (in workgroup = (frame,

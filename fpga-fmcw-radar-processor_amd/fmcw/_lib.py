@@ -26,9 +26,9 @@ MTI_OFF, MTI_2PULSE, MTI_3PULSE = 0, 2, 3
 COMPAT_CFAR, COMPAT_MTI = 1, 2
 SPEC_F32, SPEC_F16 = 0, 1
 COMM_ID_BYTES = 128
-K_RANGE, K_DOPPLER, K_CFAR2D, K_COMPACT, K_FUSED, K_COUNT = 0, 1, 2, 3, 4, 5
-KERNEL_NAMES = ("k_range", "k_doppler", "k_cfar", "k_compact", "k_fused")
-INFO_FUSED, INFO_FUSED_GROUP, INFO_FUSED_FALLBACKS, INFO_CHUNK = 1, 2, 3, 4
+K_RANGE, K_DOPPLER, K_CFAR2D, K_COMPACT, K_FUSED, K_PAIR, K_COUNT = 0, 1, 2, 3, 4, 5, 6
+KERNEL_NAMES = ("k_range", "k_doppler", "k_cfar", "k_compact", "k_fused", "k_pair")
+INFO_FUSED, INFO_FUSED_GROUP, INFO_FUSED_FALLBACKS, INFO_CHUNK, INFO_PAIR_CHUNK = 1, 2, 3, 4, 5
 
 STATUS_NAMES = {0: "FMCW_OK", -1: "FMCW_EINVAL", -2: "FMCW_ENOMEM", -3: "FMCW_EHIP",
                 -4: "FMCW_EDETCAP", -5: "FMCW_ENODEV"}

@@ -250,9 +250,11 @@ class RadarCore:
 
     def info(self, key: str) -> int:
         """fmcw_get_info: "fused" (1 = the fused range + Doppler kernel runs), "fused_group"
-        (workgroups per XCD), "fused_fallbacks", "chunk"."""
+        (workgroups per XCD), "fused_fallbacks", "chunk", "pair_chunk" (frames per chunk of the
+        paired K1 + K2 launches, 0 when they are off)."""
         k = {"fused": L.INFO_FUSED, "fused_group": L.INFO_FUSED_GROUP,
-             "fused_fallbacks": L.INFO_FUSED_FALLBACKS, "chunk": L.INFO_CHUNK}[key]
+             "fused_fallbacks": L.INFO_FUSED_FALLBACKS, "chunk": L.INFO_CHUNK,
+             "pair_chunk": L.INFO_PAIR_CHUNK}[key]
         v = C.c_int64(0)
         L.check(self._lib.fmcw_get_info(self._h, k, C.byref(v)))
         return int(v.value)

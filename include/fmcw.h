@@ -164,7 +164,8 @@ typedef enum {
   FMCW_K_CFAR2D = 2,  /* 2-D OS-CFAR */
   FMCW_K_COMPACT = 3, /* detection list ordering */
   FMCW_K_FUSED = 4,   /* K1 + K2 in one launch, spectrum resident in the XCD L2s */
-  FMCW_K_COUNT = 5
+  FMCW_K_PAIR = 5,    /* K1 of chunk c beside K2 of chunk c - 1 in one launch (double buffer) */
+  FMCW_K_COUNT = 6
 } fmcw_kernel_id;
 
 /* fmcw_get_info keys.  FMCW_INFO_FUSED: 1 when fmcw_enqueue runs the fused range + Doppler
@@ -176,7 +177,7 @@ typedef enum {
  * XCD of the fused launch.  FMCW_INFO_FUSED_FALLBACKS: fused launches that gave up (bounded
  * waits expired) and were re-run on K1 + K2 by fmcw_process. */
 typedef enum { FMCW_INFO_FUSED = 1, FMCW_INFO_FUSED_GROUP = 2, FMCW_INFO_FUSED_FALLBACKS = 3,
-               FMCW_INFO_CHUNK = 4 } fmcw_info_key;
+               FMCW_INFO_CHUNK = 4, FMCW_INFO_PAIR_CHUNK = 5 } fmcw_info_key;
 
 /* Only the functions below are exported from libfmcw.so (built -fvisibility=hidden). */
 #if defined(__GNUC__)

@@ -43,6 +43,9 @@ for s in "$@"; do
     gpu_cfar_tests) run pytest_cfar 600 python -u -m pytest tests -m gpu -v -x -k "cfar or 2d or os2d or config5 or c5 or tb" --timeout 170 --timeout-method thread -p no:cacheprovider ;;
     pmcf_c*) w=${s#pmcf_}; run "pmcf_$w" 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmcf_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
     pmcw_c*) w=${s#pmcw_}; run "pmcw_$w" 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcw_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
+    tests_pair) run pytest_pair 300 python -u -m pytest tests/test_gpu_pair.py -m gpu -v -x --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    bench_pair) FMCW_PAIR=1 run bench_pair 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
+    bench_nopair) FMCW_PAIR=0 run bench_nopair 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
     bench_generic) FMCW_K2_GENERIC=1 run bench_generic 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
     bench_quick) run bench_quick 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
     chunk_sweep)  # config-2 bench per K1/K2 chunk size (frames per launch)
