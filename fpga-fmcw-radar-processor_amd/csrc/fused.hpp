@@ -343,7 +343,7 @@ __device__ __forceinline__ void fused_doppler_role(const FusedArgs& a, int x, in
 #pragma unroll
         for (int g = 0; g < LG; ++g)
 #pragma unroll
-          for (int m = 0; m < LR; ++m) acc[g][m] = X[g][m].x * X[g][m].x + X[g][m].y * X[g][m].y;
+          for (int m = 0; m < LR; ++m) acc[g][m] = cabs2(X[g][m]);
       }
       pass_sync<false>();
       float* mrow = mags + rr * REGM;

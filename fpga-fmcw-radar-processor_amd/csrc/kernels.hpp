@@ -383,6 +383,14 @@ struct Cfar1DArgs {
 // whatever map is produced, and |X|^2 is never denormal-sensitive at these scales.  Scaling
 // the input by 2 still scales the map by exactly 2 (an even exponent shift).
 __device__ __forceinline__ float mag_sqrt(float p) { return __builtin_amdgcn_sqrtf(p); }
+// |X|^2 with both products rounded before the sum.  Left to -ffp-contract, whether x*x + y*y
+// becomes fma(x, x, y*y) depended on the surrounding code, so K2's variants and the paired
+// kernel differed in the last bit of 7 % of the cells; with contraction off in this scope every
+// kernel that computes a magnitude (K2, the fused and the paired kernels) rounds it identically.
+__device__ __forceinline__ float cabs2(float2 X) {
+#pragma clang fp contract(off)
+  return X.x * X.x + X.y * X.y;
+}
 
 constexpr int MH = 16;  // halo cells per side
 __host__ __device__ constexpr int midx(int d) { return (d + MH) + (((d + MH) >> 4) << 2); }
@@ -1088,7 +1096,7 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
 #pragma unroll
         for (int g = 0; g < LG; ++g)
 #pragma unroll
-          for (int m = 0; m < LR; ++m) acc[g][m] += X[g][m].x * X[g][m].x + X[g][m].y * X[g][m].y;
+          for (int m = 0; m < LR; ++m) acc[g][m] = rx == 0 ? cabs2(X[g][m]) : acc[g][m] + cabs2(X[g][m]);
       }
       pass_sync<false>();  // every read of the last pass is issued: the rows may be rewritten
     }

@@ -234,7 +234,7 @@ k_pair(PairArgs a) {
 #pragma unroll
       for (int g = 0; g < LG; ++g)
 #pragma unroll
-        for (int m = 0; m < LR; ++m) acc[g][m] = X[g][m].x * X[g][m].x + X[g][m].y * X[g][m].y;
+        for (int m = 0; m < LR; ++m) acc[g][m] = cabs2(X[g][m]);
       pass_sync<false>();  // every read of the last pass is issued: the rows may be rewritten
       float* mrow = mags + rr * REGM;
 #pragma unroll

@@ -45,6 +45,15 @@ for s in "$@"; do
     pmcw_c*) w=${s#pmcw_}; run "pmcw_$w" 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcw_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
     tests_pair) run pytest_pair 300 python -u -m pytest tests/test_gpu_pair.py -m gpu -v -x --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     bench_pair) FMCW_PAIR=1 run bench_pair 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
+    pair_sweep)  # paired launches: chunk sizes, and the variant libraries
+      for c in ${PCHUNKS:-24 48 72}; do
+        FMCW_PAIR=1 FMCW_PAIR_CHUNK=$c run "bench_pair_c$c" 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d
+      done
+      for lib in fpga-fmcw-radar-processor_amd/lib/var_*.so; do
+        [ -f "$lib" ] || continue
+        v=$(basename "$lib" .so)
+        FMCW_PAIR=1 FMCW_LIB="$PWD/$lib" run "bench_pair_${v#var_}" 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d
+      done ;;
     bench_nopair) FMCW_PAIR=0 run bench_nopair 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
     bench_generic) FMCW_K2_GENERIC=1 run bench_generic 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
     bench_quick) run bench_quick 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
