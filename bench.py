@@ -31,7 +31,7 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "fpga-fmcw-radar-processor_amd"))
 
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-PMC_FILE = "pmc_r02.json"  # per-launch HBM bytes from rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+PMC_FILE = "pmc_r02_s2.json"  # per-launch HBM bytes of the config-2 bench (tools/pmc_summary.py)
 
 WORKLOADS = {
     "c2": dict(ns=1024, nc=256, nrx=1, dtype="f32", cfar="os1d", frames=1024, recipe="two_targets",

@@ -921,16 +921,23 @@ __device__ __forceinline__ int xcd_block_id(int bid, int grid) {
 #ifndef FMCW_K2_WAVES     // K2 waves per SIMD asked of the register allocator (0 = by geometry)
 #define FMCW_K2_WAVES 0
 #endif
-template <int NC, int MTI>
+// FAST (below) at NC = 256 fits 128 VGPRs without scratch: 4 waves per SIMD (4 workgroups of
+// 39 KiB LDS per CU); measured K2 58.2 -> 56.0 us per 96-frame launch at config 2.  At NC = 512
+// / 1024 the fourth wave costs more than it hides (config 3 K2 41.7 -> 55.9 us, config 5 55.5
+// -> 74.6 us per launch; gpurun_out bench_libs, round 2).
+template <int NC, int MTI, bool FAST = false>
 constexpr int k2_waves() {
-  return FMCW_K2_WAVES > 0 ? FMCW_K2_WAVES : (MTI == 0 && NC <= 256 && FMCW_K2_PREFETCH <= 8) ? 3 : 2;
+  return FMCW_K2_WAVES > 0                 ? FMCW_K2_WAVES
+         : (FAST && MTI == 0 && NC == 256) ? 4
+         : (MTI == 0 && NC <= 256 && FMCW_K2_PREFETCH <= 8) ? 3
+                                                            : 2;
 }
 // FAST: the common configuration fixed at compile time -- |X| magnitude (no AMBM), no dB map,
 // and the 1-D CFAR, when enabled, at the reference geometry (8 refs / 2 guards per side, need =
 // n_ref - rank <= 4, fp32 compare).  The generic kernel keeps those as uniform runtime branches,
 // whose other arms held registers and SGPRs (spills to VGPR lanes) across the tile loop.
 template <int NC, int MTI, bool H16 = false, bool FAST = false>
-__global__ void __launch_bounds__(DopplerGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(k2_waves<NC, MTI>())))
+__global__ void __launch_bounds__(DopplerGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(k2_waves<NC, MTI, FAST>())))
 k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, int ns, int nrx,
           int lgT, int lgRB, int n_tiles, int frame0, int tile0, float* __restrict__ lin_map,
           float* __restrict__ db_map, int mag_mode, int mti_rtl, Cfar1DArgs cf, DetSink sink) {

@@ -54,6 +54,12 @@ for s in "$@"; do
         v=$(basename "$lib" .so)
         FMCW_PAIR=1 FMCW_LIB="$PWD/$lib" run "bench_pair_${v#var_}" 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d
       done ;;
+    bench_libs)  # config-2 bench for every variant library, then the default one again
+      for lib in fpga-fmcw-radar-processor_amd/lib/var_*.so; do
+        v=$(basename "$lib" .so)
+        FMCW_LIB="$PWD/$lib" run "bench_lib_${v#var_}" 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ${BENCH_ARGS:-}
+      done
+      run bench_lib_default 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ${BENCH_ARGS:-} ;;
     bench_nopair) FMCW_PAIR=0 run bench_nopair 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
     bench_generic) FMCW_K2_GENERIC=1 run bench_generic 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
     bench_quick) run bench_quick 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
