@@ -150,6 +150,17 @@ __device__ __forceinline__ fmcw_u2v ld_u2(const void* p) {
   if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const fmcw_u2v*>(p));
   else return *reinterpret_cast<const fmcw_u2v*>(p);
 }
+// Write-through (sc1) 16-B store through a buffer descriptor: the XCD L2 forwards the line at
+// once instead of holding it dirty until the end-of-kernel write-back, which a dependent launch
+// waits for (MI355X_MICROARCH.md "boundary": + dirty bytes / 6 TB/s).  `off` in bytes.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void st_f4_wt(__amdgpu_buffer_rsrc_t r, uint32_t off, float4 x) {
+  typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+  const u4v v = {__float_as_uint(x.x), __float_as_uint(x.y), __float_as_uint(x.z), __float_as_uint(x.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16 /* sc1 */);
+}
 template <bool NT>
 __device__ __forceinline__ void st_f4(void* p, float4 x) {
   const fmcw_f4v v = {x.x, x.y, x.z, x.w};

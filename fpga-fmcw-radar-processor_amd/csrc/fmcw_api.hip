@@ -773,6 +773,8 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   ALLOC(h->win_d, c.n_doppler * sizeof(float));
   // >= one fp32 frame: fmcw_range_ct writes the fp32 spectrum through it whatever spectrum_dtype
   setup_pair(h, frame_inter);
+  // K1 addresses a launch's spectrum with 32-bit byte offsets (write-through buffer stores)
+  h->chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(h->chunk, ((size_t)1 << 32) / frame_inter - 1));
   h->inter_bytes = std::max(std::max<size_t>(h->chunk, h->pair_fn ? h->pair_chunk : 0) * frame_inter,
                             (size_t)c.n_rx * c.n_range * c.n_doppler * sizeof(float2));
   ALLOC(h->inter, h->inter_bytes);

@@ -27,6 +27,16 @@ namespace fmcw {
 #define FMCW_K1_HOLDW 2
 #endif
 
+#ifndef FMCW_K1_WT          // K1: write-through (sc1) spectrum stores (1) or plain write-back (0)
+// measured at config 2 (two boxes): K1 62.2 -> 60.5 us per 96-frame launch, 756 -> 768 k frames/s;
+// config 3 neutral
+#define FMCW_K1_WT 1
+#endif
+#ifndef FMCW_K2_MAPWT       // K2: write-through (sc1) map stores (1) or non-temporal write-back (0)
+// measured at config 2: K2 55.5 -> 59.5 us per launch with write-through map stores
+#define FMCW_K2_MAPWT 0
+#endif
+
 #ifndef FMCW_CFAR1D_WHOLE   // 1-D screen over the lane's whole window (1) or two 8-cell halves (0)
 #define FMCW_CFAR1D_WHOLE 1
 #endif
@@ -234,6 +244,8 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
     float2* dst = inter + dbase;
     uint2* dst16 = reinterpret_cast<uint2*>(reinterpret_cast<uint32_t*>(inter) + dbase);
     const size_t dstep = (size_t)CI * ncb * (RB * T);
+    // FMCW_K1_WT: write-through stores (the launch's spectrum is < 4 GiB: fmcw_create caps the chunk)
+    const __amdgpu_buffer_rsrc_t wrs = wt_rsrc(inter, 0xffffffffu);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       float2 v0, v1;
@@ -245,6 +257,7 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
         v1 = lds[(c0 + 1) * REG + pad16(r0 + i * (N / 8))];
       }
       if constexpr (H16) dst16[i * dstep / 2] = make_uint2(pack_h2(v0.x, v0.y), pack_h2(v1.x, v1.y));
+      else if constexpr (FMCW_K1_WT) st_f4_wt(wrs, (uint32_t)((dbase + i * dstep) * sizeof(float2)), make_float4(v0.x, v0.y, v1.x, v1.y));
       else st_f4<FMCW_NT_SPEC_ST>(dst + i * dstep, make_float4(v0.x, v0.y, v1.x, v1.y));
     }
   }
@@ -1125,6 +1138,7 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
 
     // map store: WR*NC = 1024 floats contiguous at [f][r0][0], 16 B per lane
     {
+      const __amdgpu_buffer_rsrc_t mrs = wt_rsrc(lin_map, 0xffffffffu);  // a launch's map < 4 GiB
       constexpr int Q = WR * NC / 4 / 64;
       const size_t mbase = ((size_t)f * ns + r0) * NC;
       const int lane = opaque(lane0);
@@ -1133,7 +1147,10 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
         const int e = 4 * (lane + 64 * i);
         const int rl = e / NC, d = e - rl * NC;
         const float4 v = *reinterpret_cast<const float4*>(mags + rl * REGM + midx(d));
-        if (lin_map) st_f4<FMCW_NT_MAP>(lin_map + mbase + e, v);
+        if (lin_map) {
+          if constexpr (FMCW_K2_MAPWT) st_f4_wt(mrs, (uint32_t)((mbase + e) * sizeof(float)), v);
+          else st_f4<FMCW_NT_MAP>(lin_map + mbase + e, v);
+        }
         if (!FAST && db_map) {
           const float k = 6.0205999132796239f;  // 20 / log2(10)
           *reinterpret_cast<float4*>(db_map + mbase + e) =
