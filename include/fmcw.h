@@ -53,8 +53,10 @@
 extern "C" {
 #endif
 
-#define FMCW_ABI_VERSION 3  /* 2: fmcw_config grew compat_rtl, range_shift (27 words, 108 B);
-                               3: + spectrum_dtype (28 words, 112 B) */
+#define FMCW_ABI_VERSION 4  /* 2: fmcw_config grew compat_rtl, range_shift (27 words, 108 B);
+                               3: + spectrum_dtype (28 words, 112 B);
+                               4: FMCW_K_COUNT 5 -> 6 (fmcw_kernel_times fills 6 entries),
+                                  FMCW_INFO_PAIR_CHUNK */
 
 typedef enum {
   FMCW_OK = 0,
@@ -112,7 +114,9 @@ typedef struct fmcw_config {
   uint32_t cfar2d_scale_override; /* cfar_scale_ovr port; 0 = adaptive */
   /* resources */
   uint32_t max_frames;     /* largest n_frames per call (scratch is sized for it) */
-  uint32_t chunk_frames;   /* frames per internal kernel chunk (0 = auto) */
+  uint32_t chunk_frames;   /* frames per internal kernel chunk (0 = auto: a chunk's corner-turned
+                            * spectrum within ~192 MiB of the 256 MiB Infinity Cache, rounded to
+                            * whole rounds of the persistent grids; 96 frames at 1024 x 256) */
   int32_t device_id;       /* HIP device ordinal */
   /* RTL-compat arithmetic, a bitmask of fmcw_compat; 0 = the fp32 build spec */
   uint32_t compat_rtl;
@@ -175,7 +179,10 @@ typedef enum {
  * spectrum <= 2 MiB, a supported (n_range, n_doppler), and a placement check of the launch on
  * this device; environment FMCW_FUSED=0 disables it.  FMCW_INFO_FUSED_GROUP: workgroups per
  * XCD of the fused launch.  FMCW_INFO_FUSED_FALLBACKS: fused launches that gave up (bounded
- * waits expired) and were re-run on K1 + K2 by fmcw_process. */
+ * waits expired) and were re-run on K1 + K2 by fmcw_process.  FMCW_INFO_CHUNK: frames per
+ * K1 -> K2 chunk.  FMCW_INFO_PAIR_CHUNK: frames per chunk of the paired launches (K1 of chunk c
+ * beside K2 of chunk c - 1, double-buffered; opt-in with environment FMCW_PAIR=1 at
+ * fmcw_create, one rx, MTI off, |X|, no dB map, no 2-D CFAR, 1024 x 256), 0 when they are off. */
 typedef enum { FMCW_INFO_FUSED = 1, FMCW_INFO_FUSED_GROUP = 2, FMCW_INFO_FUSED_FALLBACKS = 3,
                FMCW_INFO_CHUNK = 4, FMCW_INFO_PAIR_CHUNK = 5 } fmcw_info_key;
 

@@ -43,7 +43,7 @@ def test_gfx950_code_object_present(lib_built):
 
 def test_struct_layouts():
     assert C.sizeof(L.FmcwDet) == 16
-    assert C.sizeof(L.FmcwConfig) == 28 * 4          # ABI 3 (fmcw.h FMCW_ABI_VERSION)
+    assert C.sizeof(L.FmcwConfig) == 28 * 4          # ABI 3/4 (fmcw.h FMCW_ABI_VERSION)
     assert L.FmcwDet.range.offset == 4 and L.FmcwDet.mag.offset == 8
 
 
@@ -57,7 +57,7 @@ def test_defaults_mirror_radar_core(lib_built):
             cfg.cfar2d_scale_max, cfg.cfar2d_scale_override) == (75, 2, 4, 6, 0)
     assert (cfg.cfar1d_ref, cfg.cfar1d_guard, cfg.cfar1d_rank) == (8, 2, 12)
     assert cfg.cfar1d_alpha == 4.0
-    assert lib_built.fmcw_abi_version() == 3
+    assert lib_built.fmcw_abi_version() == 4
     assert (cfg.compat_rtl, cfg.range_shift, cfg.spectrum_dtype) == (0, 0, L.SPEC_F32)
     assert b"gfx950" in lib_built.fmcw_version()
 
