@@ -32,6 +32,9 @@ namespace fmcw {
 // config 3 neutral
 #define FMCW_K1_WT 1
 #endif
+#ifndef FMCW_K2_BUFLD       // K2 prefetch through buffer loads with SGPR offsets (1) or global loads (0)
+#define FMCW_K2_BUFLD 1
+#endif
 #ifndef FMCW_K2_MAPWT       // K2: write-through (sc1) map stores (1) or non-temporal write-back (0)
 // measured at config 2: K2 55.5 -> 59.5 us per launch with write-through map stores
 #define FMCW_K2_MAPWT 0
@@ -1019,6 +1022,7 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
            off_of((uint32_t)(ru >> lgRB) << lgncb, (uint32_t)(ru & ((1 << lgRB) - 1)), 0);
   };
   float2 nxt[PF ? NPF : 1];
+  const __amdgpu_buffer_rsrc_t srs = wt_rsrc(const_cast<SE*>(inter), 0xffffffffu);  // FMCW_K2_BUFLD
   // last-pass twiddle bases, once per lane (NC = 256: pass 1 + one radix-16 pass, k = t)
   constexpr bool TWH = NC / 16 <= 16 && P % 16 == 0;
   GroupTwiddles<NC / 16, NC> twh;
@@ -1032,7 +1036,19 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
           const SE* pb = p + ((((uint32_t)tq >> lgT) << lgRB) << lgT) + ((uint32_t)tq & (uint32_t)(T - 1));
           const uint32_t S = (uint32_t)(P >> lgT) << (lgRB + lgT);
 #pragma unroll
-          for (int m = 0; m < NPF; ++m) nxt[m] = ld_spec<FMCW_NT_SPEC_LD>(pb + (size_t)m * S, sscale);
+          for (int m = 0; m < NPF; ++m) {
+            if constexpr (!H16 && FMCW_K2_BUFLD) {
+              // buffer load: lane offset in a VGPR, the uniform m S in an SGPR (no 64-bit VALU
+              // address add per load; the chunk's spectrum is < 4 GiB, fmcw_create caps it)
+              const uint32_t vo = (uint32_t)((const char*)pb - (const char*)inter);
+              typedef float f2v __attribute__((ext_vector_type(2)));
+              const f2v r = __builtin_bit_cast(
+                  f2v, __builtin_amdgcn_raw_buffer_load_b64(srs, vo, (uint32_t)m * S * (uint32_t)sizeof(SE), 0));
+              nxt[m] = make_float2(r.x, r.y);
+            } else {
+              nxt[m] = ld_spec<FMCW_NT_SPEC_LD>(pb + (size_t)m * S, sscale);
+            }
+          }
         } else {
 #pragma unroll
           for (int m = 0; m < NPF; ++m) {
@@ -1098,8 +1114,11 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
         for (int m = 0; m < 16; ++m) d[m] = v[m];
       }
       pass_sync<false>();
-      if (rx + 1 < nrx) prefetch(tile, rx + 1);
-      else prefetch(tile + tile_step, 0);
+      {
+        // one prefetch site: two (one per branch) merged their register results through copies
+        const bool same = rx + 1 < nrx;
+        prefetch(same ? tile : tile + tile_step, same ? rx + 1 : 0);
+      }
       float2 X[LG][LR];
       if constexpr (TWH) stockham_last_tw<NC, 16, P>(buf, t, X, twh);
       else stockham_to_regs<NC, 16, P, false>(buf, t, X);
