@@ -29,7 +29,7 @@ namespace fmcw {
 
 #ifndef FMCW_K1_WT          // K1: write-through (sc1) spectrum stores (1) or plain write-back (0)
 // measured at config 2 (two boxes): K1 62.2 -> 60.5 us per 96-frame launch, 756 -> 768 k frames/s;
-// config 3 neutral
+// config 3 neutral; config 5 (N = 8192) K1 64.9 -> 68.5 us per launch, so N <= 4096 only
 #define FMCW_K1_WT 1
 #endif
 #ifndef FMCW_K2_BUFLD       // K2 prefetch through buffer loads with SGPR offsets (1) or global loads (0)
@@ -260,7 +260,7 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
         v1 = lds[(c0 + 1) * REG + pad16(r0 + i * (N / 8))];
       }
       if constexpr (H16) dst16[i * dstep / 2] = make_uint2(pack_h2(v0.x, v0.y), pack_h2(v1.x, v1.y));
-      else if constexpr (FMCW_K1_WT) st_f4_wt(wrs, (uint32_t)((dbase + i * dstep) * sizeof(float2)), make_float4(v0.x, v0.y, v1.x, v1.y));
+      else if constexpr (FMCW_K1_WT && N <= 4096) st_f4_wt(wrs, (uint32_t)((dbase + i * dstep) * sizeof(float2)), make_float4(v0.x, v0.y, v1.x, v1.y));
       else st_f4<FMCW_NT_SPEC_ST>(dst + i * dstep, make_float4(v0.x, v0.y, v1.x, v1.y));
     }
   }
