@@ -139,8 +139,29 @@ struct RangeInfo {
   int T, RB, NT;
 };
 
+template <int N>
+RangeFn range2_fn(int dtype) {
+  if constexpr (RangeGeom<N>::T == 2 && RangeGeom<N>::P >= 128) {
+    switch (dtype) {
+      case FMCW_IN_F32: return k_range2<N, LoadF32>;
+      case FMCW_IN_F16: return k_range2<N, LoadF16>;
+      case FMCW_IN_I16: return k_range2<N, LoadI16>;
+    }
+  }
+  return nullptr;
+}
+
 RangeInfo range_info(uint32_t n, int dtype, int window = FMCW_WIN_HAMMING, bool h16 = false) {
   const bool q15 = window == FMCW_WIN_Q15_RTL;
+  // the dual range kernel (kernels.hpp k_range2): T = 2 geometries from FMCW_K1_DUAL up, fp32
+  // window, fp32 spectrum; one thread per (16 points of both chirps)
+  if (FMCW_K1_DUAL && n >= (uint32_t)FMCW_K1_DUAL && !q15 && !h16 && !std::getenv("FMCW_K1_SINGLE")) {
+    switch (n) {
+#define R2_(N) case N: if (RangeFn f = range2_fn<N>(dtype)) return {f, RangeGeom<N>::T, RangeGeom<N>::RB, RangeGeom<N>::P}; break;
+      R2_(2048) R2_(4096) R2_(8192)
+#undef R2_
+    }
+  }
   switch (n) {
 #define R_(N) case N: return {range_fn<N>(dtype, q15, h16), RangeGeom<N>::T, RangeGeom<N>::RB, RangeGeom<N>::NT};
     R_(64) R_(128) R_(256) R_(512) R_(1024) R_(2048) R_(4096) R_(8192)

@@ -267,6 +267,123 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
 }
 
 // --------------------------------------------------------------------------------------
+// K1 for T = 2 (N >= 2048), "dual": every thread carries the same 16 points of BOTH chirps of
+// the group (N / 16 threads instead of 2 N / 16), so the twiddles of a pass serve two
+// transforms, and the last pass ends in registers with X0[d] and X1[d] in the same lane -- the
+// 16-B (chirp 0, chirp 1) element of the tiled spectrum at range bin d -- so the tiles are
+// stored straight from registers: no transposing LDS read, one barrier pair fewer.  Lanes of a
+// wave hold consecutive d, so each store instruction writes whole 1 KiB tiles.
+// --------------------------------------------------------------------------------------
+#ifndef FMCW_K1_DUAL       // smallest N that runs the dual kernel (0: never)
+#define FMCW_K1_DUAL 4096
+#endif
+template <int N, typename LD>
+__global__ void __launch_bounds__(N / 16) __attribute__((amdgpu_waves_per_eu(1)))
+k_range2(const void* __restrict__ cube, float2* __restrict__ inter, const float* __restrict__ win,
+         const float* __restrict__ chirp_w, int nc, int n_groups, float /* q15_scale: unused */) {
+  using Gm = RangeGeom<N>;
+  constexpr int P = Gm::P, RB = Gm::RB, REG = Gm::REG;
+  static_assert(Gm::T == 2 && P >= 128, "two chirps per group, several waves per transform");
+  constexpr int T = 2;
+  __shared__ __attribute__((aligned(16))) float2 lds[T * REG];
+  float2* const buf0 = lds;
+  float2* const buf1 = lds + REG;
+  const int t0 = threadIdx.x;
+  const int ncb = nc / T;
+
+  typename LD::Raw a0[8], a1[8];
+  float cw0 = 1.f, cw1 = 1.f;
+  auto fetch = [&](int g) {
+    const int fr = g / ncb;
+    const int cb = g - fr * ncb;
+    const size_t chirp = (size_t)fr * nc + (size_t)cb * T;
+    const int t = opaque(t0);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      a0[m] = LD::fetch(cube, chirp * N + 2 * t + (N / 8) * m);
+      a1[m] = LD::fetch(cube, (chirp + 1) * N + 2 * t + (N / 8) * m);
+    }
+    if (chirp_w) {
+      cw0 = chirp_w[__builtin_amdgcn_readfirstlane(cb * T)];
+      cw1 = chirp_w[__builtin_amdgcn_readfirstlane(cb * T + 1)];
+    }
+  };
+  float2 wh[8];  // range window, held
+#pragma unroll
+  for (int m = 0; m < 8; ++m) wh[m] = *reinterpret_cast<const float2*>(win + 2 * t0 + (N / 8) * m);
+#pragma unroll
+  for (int m = 0; m < 8; ++m) asm volatile("" ::"v"(wh[m].x), "v"(wh[m].y));
+  int g = blockIdx.x;
+  if (g < n_groups) fetch(g);
+
+  for (; g < n_groups; g += gridDim.x) {
+    const int fr = g / ncb;
+    const int cb = g - fr * ncb;
+    const int t = opaque(t0);
+    __syncthreads();  // the previous group's last-pass reads are done with lds
+    // pass 0: radix 8 from registers, both chirps
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      float4 ax[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) ax[m] = LD::expand(q ? a1[m] : a0[m]);
+      const float cw = q ? cw1 : cw0;
+      float2* buf = q ? buf1 : buf0;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        float2 v[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          const float we = (e ? wh[m].y : wh[m].x) * cw;
+          v[m] = e ? make_float2(ax[m].z * we, ax[m].w * we) : make_float2(ax[m].x * we, ax[m].y * we);
+        }
+        Dft<8>::run(v);
+        float2* d = buf + pad16((2 * t + e) * 8);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) d[m] = v[m];
+      }
+    }
+    if (g + (int)gridDim.x < n_groups) fetch(g + gridDim.x);
+    __syncthreads();
+    // LDS passes of radix 16 while more than 16 points remain after them, both chirps at once
+    dual_passes<N, 8, P>(buf0, buf1, t);
+    // last pass in registers, then the tile stores: lane t holds range bins d = j + m N / R
+    constexpr int L = N / FinalRadix<N, 8>::R;
+    constexpr int R = FinalRadix<N, 8>::R;
+    constexpr int G = N / R / P;
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) {
+      const int j = t + P * gg;
+      float2 x0[R], x1[R];
+      const float2* s0 = buf0 + pad16(j);
+      const float2* s1 = buf1 + pad16(j);
+#pragma unroll
+      for (int m = 0; m < R; ++m) {
+        x0[m] = s0[padoff(m * (N / R))];
+        x1[m] = s1[padoff(m * (N / R))];
+      }
+      GroupTwiddles<R, N> tw;
+      tw.init(j & (L - 1));
+#pragma unroll
+      for (int m = 1; m < R; ++m) {
+        const float2 w = tw.pow(m);
+        x0[m] = cmul(x0[m], w);
+        x1[m] = cmul(x1[m], w);
+      }
+      Dft<R>::run(x0);
+      Dft<R>::run(x1);
+      const size_t fbase = (size_t)fr * N * nc;
+#pragma unroll
+      for (int m = 0; m < R; ++m) {
+        const int d = j + m * (N / R);
+        const size_t off = fbase + ((size_t)(d / RB) * ncb + cb) * (RB * T) + (size_t)(d % RB) * T;
+        st_f4<FMCW_NT_SPEC_ST>(inter + off, make_float4(x0[m].x, x0[m].y, x1[m].x, x1[m].y));
+      }
+    }
+  }
+}
+
+// --------------------------------------------------------------------------------------
 // Detection sink shared by the CFAR kernels.  Tile `wg` (a workgroup's unit: frame, range
 // rows) writes its detections, in (range, doppler) order, to its own fixed slot
 // scratch[wg * slot_cap ...] -- no atomic, no round trip.  Only a tile with more than
