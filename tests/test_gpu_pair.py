@@ -1,5 +1,6 @@
-"""GPU parity of the paired K1 + K2 launches (csrc/pair.hpp, default at BASELINE config 2's
-geometry): launch i runs the range stage of chunk i beside the Doppler stage of chunk i - 1 on
+"""GPU parity of the round-2 session-2 kernel variants: the dual-chirp range kernel (k_range2,
+default for N >= 4096) against the one-chirp kernel, and the paired K1 + K2 launches
+(csrc/pair.hpp, opt-in at BASELINE config 2's geometry): launch i runs the range stage of chunk i beside the Doppler stage of chunk i - 1 on
 double-buffered spectra.  The arithmetic is k_range's and k_doppler's, so maps and detection
 lists must be bit-identical to the serial K1 -> K2 path (FMCW_PAIR=0), and on parity with the
 oracle (maps within 1e-4 per frame, detections bit-exact against the oracle CFAR on the map)."""
@@ -75,3 +76,31 @@ def test_pair_repeated_enqueues_device_buffers(monkeypatch):
         np.testing.assert_array_equal(d, d0[d0["frame"] < nfr])
     for f in range(8, F):
         np.testing.assert_array_equal(m0[f], m0[f % 8])
+
+
+@pytest.mark.parametrize("ns,nc,dtype,mti", [
+    (4096, 64, "f32", 0),
+    (4096, 32, "i16", 3),   # MTI on: the Doppler window is not folded into the range stage
+    (8192, 32, "f16", 0),
+    (8192, 64, "i16", 2),
+])
+def test_dual_range_kernel_matches_single(monkeypatch, ns, nc, dtype, mti):
+    """K1's dual-chirp kernel (k_range2, T = 2 geometries: both chirps per thread, tiles stored
+    from registers) is bit-identical to the one-chirp-per-thread kernel (FMCW_K1_SINGLE=1): the
+    same passes in the same order.  Checked on the full map and the CFAR detections."""
+    nf = 2
+    cube = synth.frames(nf, ns, nc, 1, "two_targets", dtype=dtype, seed=11)
+    outs = []
+    for single in ("0", "1"):
+        if single == "1":
+            monkeypatch.setenv("FMCW_K1_SINGLE", "1")
+        else:
+            monkeypatch.delenv("FMCW_K1_SINGLE", raising=False)
+        with RadarCore(N_RANGE=ns, N_DOPPLER=nc, in_dtype=dtype, cfar="os1d", max_frames=nf,
+                       mti_bypass=mti == 0, NOTCH_MODE=mti or 2) as core:
+            outs.append(core.process(cube))
+    np.testing.assert_array_equal(outs[0].rd_map, outs[1].rd_map)
+    np.testing.assert_array_equal(outs[0].dets, outs[1].dets)
+    for f in range(nf):
+        ref = O.process(to_complex(cube[f], dtype), None, mti_mode=mti)["mag"]
+        check_map(outs[0].rd_map[f:f + 1], ref[None])
