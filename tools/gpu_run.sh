@@ -35,6 +35,10 @@ for s in "$@"; do
         FMCW_LIB="$PWD/$lib" run "ablib_${v#var_}" 300 python tools/ablate.py ${ABLATE_ARGS:-}
       done ;;
     cfar2d) run cfar2d 300 python tools/cfar2d_bench.py ${CFAR2D_ARGS:-} ;;
+    cfar2d_steps)  # k_cfar2d alone per strip length (FMCW_CFAR2D_STEPS; 0 = cost model)
+      for st in ${STEPS:-0 16 64 128}; do
+        FMCW_CFAR2D_STEPS=$st run "cfar2d_steps$st" 300 python tools/cfar2d_bench.py ${CFAR2D_ARGS:-}
+      done ;;
     cfar2d_libs)  # the standalone 2-D CFAR timing for every variant build
       for lib in fpga-fmcw-radar-processor_amd/lib/var_*.so; do
         v=$(basename "$lib" .so)
