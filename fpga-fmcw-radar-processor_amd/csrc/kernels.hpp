@@ -1160,7 +1160,8 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
               const uint32_t vo = (uint32_t)((const char*)pb - (const char*)inter);
               typedef float f2v __attribute__((ext_vector_type(2)));
               const f2v r = __builtin_bit_cast(
-                  f2v, __builtin_amdgcn_raw_buffer_load_b64(srs, vo, (uint32_t)m * S * (uint32_t)sizeof(SE), 0));
+                  f2v, __builtin_amdgcn_raw_buffer_load_b64(srs, vo, (uint32_t)m * S * (uint32_t)sizeof(SE),
+                                                            FMCW_NT_SPEC_LD ? 2 /* nt */ : 0));
               nxt[m] = make_float2(r.x, r.y);
             } else {
               nxt[m] = ld_spec<FMCW_NT_SPEC_LD>(pb + (size_t)m * S, sscale);
