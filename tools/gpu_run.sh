@@ -64,6 +64,7 @@ for s in "$@"; do
         FMCW_LIB="$PWD/$lib" run "bench_lib_${v#var_}" 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ${BENCH_ARGS:-}
       done
       run bench_lib_default 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ${BENCH_ARGS:-} ;;
+    bench_f16) run bench_f16 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d --spectrum f16 ;;
     single_c5) FMCW_K1_SINGLE=1 run single_c5 300 python bench.py --workload c5 --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
     bench_nopair) FMCW_PAIR=0 run bench_nopair 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
     bench_generic) FMCW_K2_GENERIC=1 run bench_generic 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
