@@ -22,6 +22,20 @@ def test_header_and_binding_agree():
     assert declared_functions() == sorted(L.SIGNATURES)
 
 
+def test_header_enums_match_binding():
+    """Kernel ids and info keys: the ctypes constants are the header's (ABI 4 grew FMCW_K_PAIR,
+    so fmcw_kernel_times fills FMCW_K_COUNT = 6 entries, and FMCW_INFO_PAIR_CHUNK)."""
+    src = L.HEADER_PATH.read_text()
+    enum = {k: int(v) for k, v in re.findall(r"\b(FMCW_(?:K|INFO)_[A-Z0-9_]+)\s*=\s*(\d+)", src)}
+    assert enum["FMCW_K_COUNT"] == L.K_COUNT == len(L.KERNEL_NAMES)
+    for i, name in enumerate(L.KERNEL_NAMES):
+        key = {"k_range": "FMCW_K_RANGE", "k_doppler": "FMCW_K_DOPPLER", "k_cfar": "FMCW_K_CFAR2D",
+               "k_compact": "FMCW_K_COMPACT", "k_fused": "FMCW_K_FUSED", "k_pair": "FMCW_K_PAIR"}[name]
+        assert enum[key] == i
+    assert enum["FMCW_INFO_CHUNK"] == L.INFO_CHUNK and enum["FMCW_INFO_PAIR_CHUNK"] == L.INFO_PAIR_CHUNK
+    assert re.search(r"#define FMCW_ABI_VERSION 4\b", src)
+
+
 def test_library_exports_every_symbol(lib_built):
     out = subprocess.run(["nm", "-D", "--defined-only", str(L.LIB_PATH)], capture_output=True,
                          text=True, check=True).stdout
