@@ -58,6 +58,8 @@ struct fmcw_handle {
   int n_cu = 256;
   // range kernel geometry (runtime copies of RangeGeom<N>)
   int T = 0, RB = 0, lgT = 0, lgRB = 0;
+  bool k1_dual = true;     // K1 may use the dual-chirp kernel (fixed at fmcw_create)
+  bool k2_fast = false;    // K2 runs its FAST instantiation (fixed at fmcw_create)
   uint32_t chunk = 1;
   // device buffers
   float* win_r = nullptr;  // [ns]
@@ -151,11 +153,12 @@ RangeFn range2_fn(int dtype) {
   return nullptr;
 }
 
-RangeInfo range_info(uint32_t n, int dtype, int window = FMCW_WIN_HAMMING, bool h16 = false) {
+RangeInfo range_info(uint32_t n, int dtype, int window = FMCW_WIN_HAMMING, bool h16 = false, bool dual = true) {
   const bool q15 = window == FMCW_WIN_Q15_RTL;
   // the dual range kernel (kernels.hpp k_range2): T = 2 geometries from FMCW_K1_DUAL up, fp32
-  // window, fp32 spectrum; one thread per (16 points of both chirps)
-  if (FMCW_K1_DUAL && n >= (uint32_t)FMCW_K1_DUAL && !q15 && !h16 && !std::getenv("FMCW_K1_SINGLE")) {
+  // window, fp32 spectrum; one thread per (16 points of both chirps).  `dual` = the handle's
+  // choice at fmcw_create (environment FMCW_K1_SINGLE=1 turns it off for A/B runs)
+  if (FMCW_K1_DUAL && dual && n >= (uint32_t)FMCW_K1_DUAL && !q15 && !h16) {
     switch (n) {
 #define R2_(N) case N: if (RangeFn f = range2_fn<N>(dtype)) return {f, RangeGeom<N>::T, RangeGeom<N>::RB, RangeGeom<N>::P}; break;
       R2_(2048) R2_(4096) R2_(8192)
@@ -653,7 +656,7 @@ void setup_pair(fmcw_handle* h, size_t frame_inter) {
   const char* env = std::getenv("FMCW_PAIR");
   if (!(env ? env[0] == '1' : kPairDefault)) return;
   if (c.n_rx != 1 || c.window == FMCW_WIN_Q15_RTL || c.spectrum_dtype != FMCW_SPEC_F32 ||
-      c.cfar_kind == FMCW_CFAR_OS2D || !k2_fast(c))
+      c.cfar_kind == FMCW_CFAR_OS2D || !h->k2_fast)
     return;
   const PairFn fn = pair_fn(c.n_range, c.n_doppler, c.in_dtype);
   if (!fn) return;
@@ -752,7 +755,9 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   h->cfg = *cfg;
   const fmcw_config& c = h->cfg;
   h->n_cu = prop.multiProcessorCount;
-  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, c.spectrum_dtype == FMCW_SPEC_F16);
+  h->k1_dual = !std::getenv("FMCW_K1_SINGLE");
+  h->k2_fast = k2_fast(c);
+  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, c.spectrum_dtype == FMCW_SPEC_F16, h->k1_dual);
   h->T = ri.T;
   h->RB = ri.RB;
   h->lgT = __builtin_ctz(ri.T);
@@ -763,7 +768,7 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
 #ifdef FMCW_K1_GRID_PER_CU  // tuning switch (tools/build_variants.sh): K1 workgroups per CU
   h->grid_range = std::min(h->grid_range, FMCW_K1_GRID_PER_CU * h->n_cu);
 #endif
-  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype == FMCW_SPEC_F16, k2_fast(c));
+  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype == FMCW_SPEC_F16, h->k2_fast);
   occupancy_grid(di.fn, di.NT, 0, h->n_cu, &h->grid_doppler);
   // two-stream pipeline of chunks (FMCW_PIPE=1): ring of FMCW_PIPE_BUFS intermediate buffers of
   // FMCW_PIPE_CHUNK frames, sized so the ring stays in the 256 MiB Infinity Cache
@@ -907,8 +912,8 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
     return fail(FMCW_EINVAL, "n_dets_dev is required when a CFAR is configured");
   HIP_TRY(hipSetDevice(c.device_id));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, c.spectrum_dtype == FMCW_SPEC_F16);
-  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype == FMCW_SPEC_F16, k2_fast(c));
+  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, c.spectrum_dtype == FMCW_SPEC_F16, h->k1_dual);
+  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype == FMCW_SPEC_F16, h->k2_fast);
   const size_t frame_px = (size_t)c.n_range * c.n_doppler;
   const size_t in_frame_bytes = cube_bytes(c, 1);
   const Cfar1DArgs cf1 = cfar1_args(c);
@@ -1131,7 +1136,7 @@ int fmcw_range_ct(fmcw_handle* h, const void* cube, size_t n_frames, void* spec,
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // the stage output is the fp32 spectrum whatever spectrum_dtype the path uses: K1's fp32
   // variant, as many frames per launch as the intermediate buffer holds at 8 B per point
-  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, false);
+  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, false, h->k1_dual);
   const size_t in_frame_bytes = cube_bytes(c, 1);
   const size_t fr_px = (size_t)c.n_rx * c.n_range * c.n_doppler;
   const size_t rc_chunk = std::max<size_t>(1, h->inter_bytes / (fr_px * sizeof(float2)));
