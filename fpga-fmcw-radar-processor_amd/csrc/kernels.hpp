@@ -1049,7 +1049,8 @@ __device__ __forceinline__ int xcd_block_id(int bid, int grid) {
 #define FMCW_K2_ORDER 1
 #endif
 #ifndef FMCW_K2_PF_NC     // K2: largest NC with the next-unit register prefetch
-#define FMCW_K2_PF_NC 256  // measured: no gain at NC = 512, 1024 (profiles/r02/k2_pf)
+#define FMCW_K2_PF_NC 256  // measured: no gain at NC = 512, 1024 (profiles/r02/k2_pf); again after
+                           // the one-site prefetch: NC 512 41.0 vs 41.2 us, NC 1024 62.8 vs 55.4 us
 #endif
 #ifndef FMCW_K2_WAVES     // K2 waves per SIMD asked of the register allocator (0 = by geometry)
 #define FMCW_K2_WAVES 0
