@@ -3,11 +3,15 @@
 
 One step = one pass of the hot path (window -> range FFT -> corner turn -> Doppler FFT ->
 |X| map -> OS-CFAR -> ordered detection list) over one batch of synthetic frames already
-resident in HBM.  Workload at N=1: BASELINE config 2 -- 256 chirps x 1024 samples, fp32
-complex, 1 Rx, 1-D OS-CFAR 16 ref / 4 guard -- in batches of 1024 frames per GPU per step
+resident in HBM.  Headline workload at N=1: BASELINE config 2 -- 256 chirps x 1024 samples,
+fp32 complex, 1 Rx, 1-D OS-CFAR 16 ref / 4 guard -- in batches of 1024 frames per GPU per step
 (= config 4's per-GPU share of 8192 frames at 8 GPUs; weak scaling).  With N > 1 each rank
 processes its own 1024 frames (frame sharding, no data-path collective) and the detection
 lists are gathered over RCCL inside the step (config 4).
+
+The same JSON line carries sub-records "config3" and "config5" (BASELINE configs 3 and 5, 16
+frames per GPU per step, 2-D OS-CFAR), timed the same way in the same process, each with the
+roofline of ITS dominant kernel (the kernel with the most time per step).
 
 Launch: `python bench.py [--gpus N --steps K --warmup W]`, or for N > 1
 `python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
@@ -15,8 +19,10 @@ Launch: `python bench.py [--gpus N --steps K --warmup W]`, or for N > 1
 
 roofline: the dominant kernel's algorithmic bytes per launch / its average launch duration,
 from HIP events the library records on the launch stream (fmcw_set_profiling) over a
-profiled repeat of the timed steps; traffic from profiles/pmc_<round>.json (rocprofv3
-FETCH_SIZE / WRITE_SIZE passes, gfx950 FETCH x2 correction) when present, else null.
+profiled repeat of the timed steps.  traffic: HBM bytes per launch from rocprofv3 PMC passes
+(profiles/pmc_r03.json, per frame x the launch's mean frames; tools/pmc_summary.py), or null.
+The 2-D CFAR (k_cfar2d) is bound by VALU issue, not bytes: its roofline is SQ_INSTS_VALU per
+launch (same profile file) / launch time against the chip's issue rate, its map bytes beside.
 """
 from __future__ import annotations
 
@@ -30,8 +36,9 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "fpga-fmcw-radar-processor_amd"))
 
-HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-PMC_FILE = "pmc_r02_s2.json"  # per-launch HBM bytes of the config-2 bench (tools/pmc_summary.py)
+HBM_PEAK_GBPS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+CLOCK_GHZ = 2.4             # MI355X peak engine clock
+PMC_FILE = "pmc_r03.json"   # per-frame HBM bytes and SQ counts per workload (tools/pmc_summary.py)
 
 WORKLOADS = {
     "c2": dict(ns=1024, nc=256, nrx=1, dtype="f32", cfar="os1d", frames=1024, recipe="two_targets",
@@ -41,6 +48,7 @@ WORKLOADS = {
     "c5": dict(ns=8192, nc=1024, nrx=1, dtype="f16", cfar="os2d", frames=16, recipe="two_targets",
                desc="BASELINE config 5: 1024 chirps x 8192 range bins, fp16 complex samples, 2-D OS-CFAR"),
 }
+SUB = {"c3": "config3", "c5": "config5"}
 
 
 def parse():
@@ -51,6 +59,7 @@ def parse():
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--frames", type=int, default=0, help="frames per GPU per step (0 = workload default)")
     ap.add_argument("--chunk", type=int, default=0, help="frames per kernel chunk (0 = library auto)")
+    ap.add_argument("--no-sub", action="store_true", help="skip the config-3 / config-5 sub-records")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-gather", action="store_true")
@@ -62,35 +71,81 @@ def parse():
     return ap.parse_args()
 
 
-def main():
-    args = parse()
+def load_pmc():
+    f = REPO / "profiles" / PMC_FILE
+    if f.exists():
+        try:
+            return json.loads(f.read_text())
+        except Exception:  # noqa: BLE001 -- a damaged file means "no counters"
+            return {}
+    return {}
+
+
+def kernel_rooflines(wl, name, F, steps, kt, spectrum, n_cu, pmc):
+    """Per-kernel rooflines from the HIP-event times of `steps` profiled steps of F frames."""
+    ns, nc, nrx = wl["ns"], wl["nc"], wl["nrx"]
+    b_in = 8 if wl["dtype"] == "f32" else 4
+    b_sp = 4 if spectrum == "f16" else 8
+    px = ns * nc * nrx
+    frames = F * steps
+    # algorithmic bytes per frame (SURVEY.md 8d): K1 cube in + spectrum out; K2 spectrum in + map
+    # out; K3 map in (+ detections, negligible)
+    alg = {"k_range": px * (b_in + b_sp), "k_doppler": px * b_sp + ns * nc * 4, "k_cfar": ns * nc * 4}
+    what = {"k_range": "k_range (window + range FFT + corner turn)",
+            "k_doppler": "k_doppler (Doppler FFT + |X|" + (" NCI" if nrx > 1 else "") + " + map"
+                         + (" + 1-D CFAR)" if wl["cfar"] == "os1d" else ")"),
+            "k_cfar": "k_cfar2d (2-D OS-CFAR, 128 refs, adaptive scale)",
+            "k_compact": "k_det_scan / k_det_copy (ordered detection list)"}
+    pw = (pmc.get("workloads") or {}).get(name, {})
+    pk = pw.get("kernels", {})
+    out = {}
+    for k, (ms, n) in kt.items():
+        if not n:
+            continue
+        per_step_ms = ms / steps
+        r = {"kernel": what.get(k, k), "launches_per_step": n // steps, "avg_launch_ms": round(ms / n, 5),
+             "ms_per_step": round(per_step_ms, 4)}
+        fpl = frames / n                                   # mean frames per launch
+        if k in alg:
+            bpl = alg[k] * fpl
+            gbps = bpl / (ms / n * 1e-3) / 1e9
+            traffic = pk.get(k, {}).get("hbm_bytes_per_frame")
+            r.update({"bound": "hbm", "achieved": round(gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                      "frac": round(gbps / HBM_PEAK_GBPS, 4), "bytes_per_launch": int(bpl),
+                      "frames_per_launch": round(fpl, 3),
+                      "traffic": int(traffic * fpl) if traffic else None})
+        if k == "k_cfar" and wl["cfar"] == "os2d":
+            # issue-bound: one VALU wave-instruction per CU per clock (4 SIMDs x one per 4 cycles)
+            hbm = dict(r)
+            sq = pk.get("k_cfar", {}).get("SQ_INSTS_VALU_per_frame")
+            peak = n_cu * CLOCK_GHZ                            # G wave-instructions / s
+            ach = sq * fpl / (ms / n * 1e-3) / 1e9 if sq else None
+            r.update({"bound": "valu", "achieved": round(ach, 1) if ach else None, "peak": round(peak, 1),
+                      "unit": "G VALU wave-instructions/s", "frac": round(ach / peak, 4) if ach else None,
+                      "SQ_INSTS_VALU_per_launch": int(sq * fpl) if sq else None,
+                      "map_GBps": hbm["achieved"], "map_frac_of_hbm": hbm["frac"],
+                      "traffic": hbm["traffic"]})
+        out[k] = r
+    return out
+
+
+def run_workload(name, args, world, rank, dev, primary, pmc, n_cu):
     import numpy as np
     import torch
     import torch.distributed as dist
     from fmcw import RadarCore, synth
     from fmcw.dist import RcclGather, gather_detections
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    wl = dict(WORKLOADS[args.workload])
-    if args.frames:
+    wl = dict(WORKLOADS[name])
+    if primary and args.frames:
         wl["frames"] = args.frames
     F, ns, nc, nrx = wl["frames"], wl["ns"], wl["nc"], wl["nrx"]
-    # one rank per GPU; the modulo only matters for a rehearsal of N ranks on fewer GPUs
-    # (with FMCW_BENCH_BACKEND=gloo, since RCCL needs distinct devices)
-    local = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        backend = os.environ.get("FMCW_BENCH_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
-
+    steps = args.steps if primary else max(3, args.steps // 2)
+    warmup = args.warmup if primary else max(1, args.warmup // 2)
+    local = dev.index
     core = RadarCore(N_RANGE=ns, N_DOPPLER=nc, N_RX=nrx, in_dtype=wl["dtype"], cfar=wl["cfar"],
-                     max_frames=F, chunk_frames=args.chunk, device=local, spectrum=args.spectrum)
+                     max_frames=F, chunk_frames=args.chunk if primary else 0, device=local,
+                     spectrum=args.spectrum if primary else "f32")
     # synthetic input: 16 distinct frames (seed 1234 + global frame), tiled to F, resident in HBM
     n_u = min(16, F)
     first_global = rank * F
@@ -103,13 +158,14 @@ def main():
     del ut
     rd_map = torch.empty((F, ns, nc), dtype=torch.float32, device=dev)
     det_cap = F * 4096
-    # two detection buffers: step i+1 may be enqueued while step i's list is still gathered
+    # two detection buffers: step i+1 may be enqueued while step i's list is still gathered;
+    # status words (fmcw.h FMCW_STATUS_WORDS): found, lost, window / word saturations
     bufs = [(torch.empty((det_cap, 4), dtype=torch.int32, device=dev), torch.zeros(4, dtype=torch.int32, device=dev))
             for _ in range(2)]
     dets, n_dets = bufs[0]
     cstream = torch.cuda.current_stream(dev)
     stream = cstream.cuda_stream
-    gather = world > 1 and not args.no_gather
+    gather = primary and world > 1 and not args.no_gather
     gather_kind = None
     rg = None
     wire_cap = F * 128                 # records per rank on the wire: 128 per frame (~64 found)
@@ -120,7 +176,7 @@ def main():
         try:
             obj = [RcclGather.make_id() if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
-            rg = RcclGather(obj[0], world, rank, local)
+            rg = RcclGather(obj[0], world, rank, local, wire_cap)
             gather_kind = "libfmcw fmcw_gather_dets (RCCL send/recv to rank 0, fixed wire_cap, no host sync)"
         except Exception as e:  # noqa: BLE001 -- reported, then the torch path is used
             print(f"rank {rank}: RCCL gather unavailable ({e}); using torch all_gather", file=sys.stderr)
@@ -137,8 +193,6 @@ def main():
     last = {"i": 0, "pending": None}
 
     def do_gather(d, nd, ev):
-        # on its own stream after step's kernels (event): the gather's device->host count reads
-        # wait for that step only; its reads of (d, nd) are complete when this returns
         with torch.cuda.stream(gstream):
             gstream.wait_event(ev)
             allr, counts = gather_detections(d, nd[:2], first_global)
@@ -155,7 +209,7 @@ def main():
             ev = torch.cuda.Event()
             ev.record(cstream)
             gstream.wait_event(ev)
-            rg.gather(d.data_ptr(), nd.data_ptr(), wire_cap, first_global,
+            rg.gather(d.data_ptr(), det_cap, nd.data_ptr(), first_global,
                       root_out.data_ptr() if rank == 0 else None, root_n.data_ptr() if rank == 0 else None,
                       0, gstream.cuda_stream)
             g_done[b] = torch.cuda.Event()
@@ -188,89 +242,51 @@ def main():
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
         return float(el.item())
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     flush()
-    elapsed = timed(args.steps)
-    n_det_step = int(n_dets[0].item())
+    elapsed = timed(steps)
+    st = n_dets.tolist()
+    n_det_step = int(st[0])
 
     # profiled repeat: per-kernel durations from HIP events on the launch stream
     core.reset_kernel_times()
     core.set_profiling(True)
-    elapsed_prof = timed(args.steps)
+    elapsed_prof = timed(steps)
     kt = core.kernel_times()
     core.set_profiling(False)
-
-    frames_total = world * F * args.steps
-    value = frames_total / elapsed
+    spectrum = args.spectrum if primary else "f32"
+    kern = kernel_rooflines(wl, name, F, steps, kt, spectrum, n_cu, pmc)
+    dom = max((k for k in kern if k in ("k_range", "k_doppler", "k_cfar")), key=lambda k: kern[k]["ms_per_step"])
+    value = world * F * steps / elapsed
     b_in = 8 if wl["dtype"] == "f32" else 4
-    px = ns * nc * nrx
-    ms_r, n_r = kt["k_range"]
-    ms_d, n_d = kt["k_doppler"]
-    b_sp = 4 if args.spectrum == "f16" else 8                       # corner-turned spectrum element
-    bytes_range = F * args.steps * px * (b_in + b_sp)              # stage A: cube in + spectrum out
-    bytes_dopp = F * args.steps * (px * b_sp + ns * nc * 4)        # spectrum in + map out
-    kern = {}
-    for name, (ms, n) in kt.items():
-        if n:
-            kern[name] = {"launches_per_step": n // args.steps, "avg_ms": ms / n}
-    if ms_r:
-        kern["k_range"]["GBps_algorithmic"] = bytes_range / (ms_r * 1e-3) / 1e9
-    if ms_d:
-        kern["k_doppler"]["GBps_algorithmic"] = bytes_dopp / (ms_d * 1e-3) / 1e9
-    ms_f, n_f = kt["k_fused"]
-    ms_p, n_p = kt["k_pair"]
-    if ms_p:
-        # paired launches (pair.hpp): K1's and K2's algorithmic bytes move in the same launches
-        kern["k_pair"]["GBps_algorithmic"] = (bytes_range + bytes_dopp) / (ms_p * 1e-3) / 1e9
-    pmc = {}
-    pmc_file = REPO / "profiles" / PMC_FILE
-    if pmc_file.exists():
-        try:
-            pmc = json.loads(pmc_file.read_text())
-        except Exception:
-            pmc = {}
-    if n_f:
-        # fused K1 + K2: the compulsory bytes (cube in, map out) per launch of the whole batch
-        bytes_fused = F * args.steps * (px * b_in + ns * nc * 4)
-        kern["k_fused"]["GBps_algorithmic"] = bytes_fused / (ms_f * 1e-3) / 1e9
-        achieved = bytes_fused / (ms_f * 1e-3) / 1e9
-        traffic = None
-        if pmc.get("workload") == args.workload and pmc.get("frames_per_launch") == F // max(1, n_f // args.steps):
-            traffic = pmc.get("k_fused_bytes_per_launch")
-        roofline = {"kernel": "k_fused (window + range FFT + corner turn in L2 + Doppler FFT + |X| + map + 1-D CFAR)",
-                    "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                    "bytes_per_launch": bytes_fused // max(1, n_f),
-                    "avg_launch_ms": round(ms_f / n_f, 5)}
-    elif n_p:
-        # range + Doppler stages in one launch: cube in + spectrum out + spectrum in + map out
-        achieved = (bytes_range + bytes_dopp) / (ms_p * 1e-3) / 1e9
-        traffic = None
-        if pmc.get("workload") == args.workload and pmc.get("frames_per_launch") == F // max(1, n_p // args.steps):
-            traffic = pmc.get("k_pair_bytes_per_launch")
-        roofline = {"kernel": "k_pair (range stage of chunk c beside the Doppler stage + |X| + map + 1-D CFAR "
-                              "of chunk c-1)", "bound": "hbm",
-                    "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                    "bytes_per_launch": (bytes_range + bytes_dopp) // max(1, n_p),
-                    "avg_launch_ms": round(ms_p / n_p, 5)}
-    else:
-        achieved = bytes_range / (ms_r * 1e-3) / 1e9 if ms_r else None
-        traffic = None
-        if pmc.get("workload") == args.workload and pmc.get("frames_per_launch") == F // max(1, n_r // args.steps):
-            traffic = pmc.get("k_range_bytes_per_launch")
-        roofline = {"kernel": "k_range (window + range FFT + corner turn)", "bound": "hbm",
-                    "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None, "traffic": traffic,
-                    "bytes_per_launch": bytes_range // max(1, n_r),
-                    "avg_launch_ms": round(ms_r / n_r, 5) if n_r else None}
-    e2e_bytes = F * (px * b_in + ns * nc * 4) + 16 * n_det_step
+    e2e_bytes = F * (ns * nc * nrx * b_in + ns * nc * 4) + 16 * n_det_step
+    rec = {
+        "metric": "radar frames/sec (range-Doppler+CFAR)",
+        "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(elapsed / steps * 1e3, 4),
+        "dtype": wl["dtype"],
+        "config": {"workload": wl["desc"], "frames_per_gpu_step": F, "n_chirps": nc,
+                   "n_samples": ns, "n_rx": nrx, "cfar": wl["cfar"], "rd_map": "linear fp32, written",
+                   "spectrum": spectrum,
+                   "detection_gather": gather_kind if gather else "none",
+                   "parallelism": f"frame-sharded x{world}"},
+        "range_kernel": core.info("range_kernel"),
+        "chunk_frames": core.info("chunk"),
+        "detections_per_step": n_det_step,
+        "status_words": [int(x) for x in st],
+        "e2e_GBps_algorithmic": round(e2e_bytes * steps * world / elapsed / 1e9, 1),
+        "e2e_frac_of_peak": round(e2e_bytes * steps / elapsed / 1e9 / HBM_PEAK_GBPS, 4),
+        "roofline": {k: v for k, v in kern[dom].items() if k not in ("launches_per_step",)},
+        "kernels": kern,
+        "profiled_step_ms": round(elapsed_prof / steps * 1e3, 4),
+    }
+    from fmcw._lib import RANGE_KERNELS
+    rec["range_kernel"] = RANGE_KERNELS[rec["range_kernel"]]
 
-    # H2D-inclusive rate: the cube streamed from pinned host memory inside each step (copy of
-    # batch i+1 on a copy stream overlapping the compute of batch i), PCIe-bound by design
-    h2d = None
-    if not args.no_h2d and world == 1:
+    if primary and not args.no_h2d and world == 1:
+        # H2D-inclusive rate: the cube streamed from pinned host memory inside each step (copy of
+        # batch i+1 on a copy stream overlapping the compute of batch i), PCIe-bound by design
         Fh = min(F, 256)
         host = torch.empty((Fh,) + tuple(cube.shape[1:]), dtype=cube.dtype, pin_memory=True)
         host.copy_(cube[:Fh].cpu())
@@ -301,89 +317,115 @@ def main():
         h2d_run()
         torch.cuda.synchronize(dev)
         th = time.perf_counter() - t0
-        h2d = {"frames_per_s_per_gpu": round(n_h * Fh / th, 1),
-               "GBps_h2d": round(n_h * host.numel() * host.element_size() / th / 1e9, 1),
-               "sample": f"{n_h} batches of {Fh} frames from pinned host memory, copy/compute overlapped"}
+        rec["h2d_inclusive"] = {"frames_per_s_per_gpu": round(n_h * Fh / th, 1),
+                                "GBps_h2d": round(n_h * host.numel() * host.element_size() / th / 1e9, 1),
+                                "sample": f"{n_h} batches of {Fh} frames from pinned host memory, copy/compute overlapped"}
         del host, dbuf
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, str(REPO / "oracle"))
-        import cpu_baseline as cb
-        import fmcw_oracle as O
-        # C backend (oracle/fmcw_cpu.c) on the same workload: single core and all allowed cores
-        nt = cb.threads_allowed()
-        batch = max(8, nt)
-        uu = synth.frames(min(16, batch), ns, nc, nrx, wl["recipe"], seed=1234, dtype="f32")
-        if wl["dtype"] != "f32":
-            uu = (uu[..., 0].astype(np.float32) + 1j * uu[..., 1].astype(np.float32)).astype(np.complex64)
-        ucube = np.concatenate([uu] * ((batch + len(uu) - 1) // len(uu)))[:batch]
-        cf = O.Cfar1D() if wl["cfar"] == "os1d" else O.Cfar2D()
-        mc = cb.measure_c(ucube, cf, runs=20, budget_s=args.cpu_seconds / 2)
-        ac = mc["all_core"]
-        cpu = {"value": round(ac["frames_per_s"], 2), "unit": "frames/s", "cores": ac["threads"],
-               "kind": "port",
-               "single_core_frames_per_s": round(mc["single_core"]["frames_per_s"], 2),
-               "nproc": mc["nproc"], "cpus_allowed": mc["affinity"], "omp_num_threads": mc["omp_num_threads"],
-               "cpu_model": mc["cpu_model"],
-               "sample": (f"C restatement of the oracle (oracle/fmcw_cpu.c, OpenMP, fp32), {batch} frames of "
-                          f"{ns}x{nc}x{nrx} per run, median of {ac['runs']} runs at {ac['threads']} threads and "
-                          f"{mc['single_core']['runs']} runs at 1 thread")}
-        if args.workload == "c2":
-            # config-3 leg (2-D OS-CFAR, 4 rx NCI): one frame per run
-            u3 = synth.frames(1, 4096, 512, 4, "two_targets", seed=1234, dtype="f32")
-            m3 = cb.measure_c(u3, O.Cfar2D(), runs=20, budget_s=args.cpu_seconds / 2)
-            cpu["config3_2d_cfar"] = {
-                "all_core_frames_per_s": round(m3["all_core"]["frames_per_s"], 3),
-                "single_core_frames_per_s": round(m3["single_core"]["frames_per_s"], 3),
-                "threads": m3["all_core"]["threads"],
-                "sample": f"1 frame of 4096x512x4 (NCI, 2-D OS-CFAR) per run, median of "
-                          f"{m3['all_core']['runs']} / {m3['single_core']['runs']} runs"}
-            # the round-1 NumPy/SciPy port, for continuity
-            uu1 = uu[:8, 0] if uu.ndim == 4 else uu[:8]
-            mp = cb.measure(ns, nc, lambda k: uu1[:k], target_s=2.0, batch=8, workers=nt)
-            cpu["numpy_port_frames_per_s"] = round(mp["frames_per_s"], 2)
-
-    out = {
-        "metric": "radar frames/sec (range-Doppler+CFAR)",
-        "value": round(value, 1),
-        "unit": "frames/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": wl["dtype"],
-        "data": "synthetic (tb_radar_core-style point targets + uniform noise, int16-quantised)",
-        "config": {"workload": wl["desc"], "frames_per_gpu_step": F, "n_chirps": nc,
-                   "n_samples": ns, "n_rx": nrx, "cfar": wl["cfar"], "rd_map": "linear fp32, written",
-                   "spectrum": args.spectrum,
-                   "detection_gather": gather_kind if gather else "none (single GPU)",
-                   "parallelism": f"frame-sharded x{world}"},
-        "e2e_GBps_algorithmic": round(e2e_bytes * args.steps * world / elapsed / 1e9, 1),
-        "e2e_frac_of_peak": round(e2e_bytes * args.steps / elapsed / 1e9 / HBM_PEAK_GBPS, 4),
-        "fused_path": bool(core.info("fused")),
-        "chunk_frames": core.info("chunk"),
-        "pair_chunk_frames": core.info("pair_chunk"),
-        "detections_per_step": n_det_step,
-        "roofline": roofline,
-        "kernels": kern,
-        "profiled_step_ms": round(elapsed_prof / args.steps * 1e3, 4),
-        "cpu_baseline": cpu,
-        "h2d_inclusive_fps": h2d["frames_per_s_per_gpu"] if h2d else None,
-        "h2d_inclusive": h2d,
-    }
     if rg is not None and rank == 0:
         torch.cuda.synchronize(dev)
-        out["config"]["gathered_records_last_step"] = int(root_n[0].item())
-        out["config"]["gather_lost_last_step"] = int(root_n[1].item())
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+        rec["config"]["gathered_records_last_step"] = int(root_n[0].item())
+        rec["config"]["gather_lost_last_step"] = int(root_n[1].item())
     core.close()
     if rg is not None:
         rg.close()
+    del cube, rd_map, bufs
+    torch.cuda.empty_cache()
+    return rec
+
+
+def cpu_baseline(args, wl):
+    import numpy as np
+    from fmcw import synth
+    sys.path.insert(0, str(REPO / "oracle"))
+    import cpu_baseline as cb
+    import fmcw_oracle as O
+    # C backend (oracle/fmcw_cpu.c) on the same workload: single core and the job's CPU share
+    ns, nc, nrx = wl["ns"], wl["nc"], wl["nrx"]
+    nt = cb.threads_allowed()
+    batch = max(8, nt)
+    uu = synth.frames(min(16, batch), ns, nc, nrx, wl["recipe"], seed=1234, dtype="f32")
+    ucube = np.concatenate([uu] * ((batch + len(uu) - 1) // len(uu)))[:batch]
+    cf = O.Cfar1D() if wl["cfar"] == "os1d" else O.Cfar2D()
+    mc = cb.measure_c(ucube, cf, runs=20, budget_s=args.cpu_seconds / 2)
+    ac = mc["all_core"]
+    cpu = {"value": round(ac["frames_per_s"], 2), "unit": "frames/s", "cores": ac["threads"],
+           "kind": "port",
+           "single_core_frames_per_s": round(mc["single_core"]["frames_per_s"], 2),
+           "nproc": mc["nproc"], "cpus_allowed": mc["affinity"], "omp_num_threads": mc["omp_num_threads"],
+           "cpu_model": mc["cpu_model"],
+           "sample": (f"C restatement of the oracle (oracle/fmcw_cpu.c, OpenMP, fp32), {batch} frames of "
+                      f"{ns}x{nc}x{nrx} per run, median of {ac['runs']} runs at {ac['threads']} threads and "
+                      f"{mc['single_core']['runs']} runs at 1 thread")}
+    # the whole node's CPUs: the job runs on a 16-CPU share of the node (gpurun box rule), so the
+    # all-affinity figure is the measured per-thread rate at 16 threads times the CPUs the
+    # affinity mask lists -- an extrapolation, labelled as such, not a measurement
+    aff = mc["affinity"] if isinstance(mc["affinity"], int) else None
+    if aff and ac["threads"] > 0:
+        cpu["all_affinity_cpus_estimate"] = {
+            "cpus": aff, "frames_per_s": round(ac["frames_per_s"] / ac["threads"] * aff, 1),
+            "how": f"{ac['threads']}-thread rate x {aff}/{ac['threads']} (linear; not run: the job's CPU share "
+                   f"is {ac['threads']} CPUs)"}
+    if args.workload == "c2":
+        # config-3 leg (2-D OS-CFAR, 4 rx NCI): one frame per run
+        u3 = synth.frames(1, 4096, 512, 4, "two_targets", seed=1234, dtype="f32")
+        m3 = cb.measure_c(u3, O.Cfar2D(), runs=20, budget_s=args.cpu_seconds / 2)
+        cpu["config3_2d_cfar"] = {
+            "all_core_frames_per_s": round(m3["all_core"]["frames_per_s"], 3),
+            "single_core_frames_per_s": round(m3["single_core"]["frames_per_s"], 3),
+            "threads": m3["all_core"]["threads"],
+            "sample": f"1 frame of 4096x512x4 (NCI, 2-D OS-CFAR) per run, median of "
+                      f"{m3['all_core']['runs']} / {m3['single_core']['runs']} runs"}
+    return cpu
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; the modulo only matters for a rehearsal of N ranks on fewer GPUs
+    # (with FMCW_BENCH_BACKEND=gloo, since RCCL needs distinct devices)
+    local = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        backend = os.environ.get("FMCW_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+    pmc = load_pmc()
+
+    rec = run_workload(args.workload, args, world, rank, dev, True, pmc, n_cu)
+    subs = {}
+    if not args.no_sub and args.workload == "c2":
+        for w in ("c3", "c5"):
+            subs[SUB[w]] = run_workload(w, args, world, rank, dev, False, pmc, n_cu)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, WORKLOADS[args.workload])
+
+    out = {
+        "metric": rec["metric"], "value": rec["value"], "unit": "frames/s", "n_gpus": world,
+        "steps": rec["steps"], "warmup": rec["warmup"], "ms_per_step": rec["ms_per_step"],
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": rec["dtype"],
+        "data": "synthetic (tb_radar_core-style point targets + uniform noise, int16-quantised)",
+        "config": rec["config"],
+        "roofline": rec["roofline"],
+        "cpu_baseline": cpu,
+    }
+    for k in ("range_kernel", "chunk_frames", "detections_per_step", "status_words", "e2e_GBps_algorithmic",
+              "e2e_frac_of_peak", "kernels", "profiled_step_ms", "h2d_inclusive"):
+        if k in rec:
+            out[k] = rec[k]
+    out["h2d_inclusive_fps"] = rec.get("h2d_inclusive", {}).get("frames_per_s_per_gpu")
+    out.update(subs)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

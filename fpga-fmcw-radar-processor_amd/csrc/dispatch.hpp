@@ -1,0 +1,56 @@
+// dispatch.hpp -- kernel selection tables of libfmcw.so.  Each table lives in its own
+// translation unit (inst_*.hip) so the template instantiations compile in parallel; the host
+// logic (fmcw_api.hip) sees only these function-pointer factories.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "kernels.hpp"
+
+namespace fmcw {
+
+// ---- K1: window + range FFT + corner turn -------------------------------------------------
+using RangeFn = void (*)(const void*, float2*, const float*, const float*, int, int, float, uint32_t*);
+// which range kernel family a handle runs (fmcw.h FMCW_INFO_RANGE_KERNEL)
+enum RangeKind { kRangeSingle = 0, kRangeDual = 1, kRangeSeq = 2 };
+struct RangeInfo {
+  RangeFn fn;
+  int T, RB, NT;   // chirps per group, range bins per 1 KiB tile, threads per workgroup
+  int kind;        // RangeKind actually selected
+};
+// want = the preferred family (kRangeSeq: k_range_sq where instantiated, else k_range2, else
+// k_range); q15 / h16 select the RTL-compat window and the fp16 spectrum (k_range only)
+RangeInfo range_info(uint32_t n, int dtype, int window, bool h16, int want);
+
+// ---- K2: Doppler window + FFT + |X| / NCI + map + 1-D CFAR --------------------------------
+using DopplerFn = void (*)(const float2*, const float*, int, int, int, int, int, int, int, float*,
+                           float*, int, int, int, Cfar1DArgs, DetSink, uint32_t*);
+struct DopplerInfo {
+  DopplerFn fn;
+  int WR, NT;  // range rows per wave tile, threads per workgroup (DopplerGeom::WPB tiles)
+};
+DopplerFn doppler_fn_f32(uint32_t nc, int mti, bool fast, bool q15);  // inst_doppler.hip
+DopplerFn doppler_fn_f16(uint32_t nc, int mti, bool fast);            // inst_doppler_h16.hip
+inline DopplerInfo doppler_info(uint32_t nc, int mti = FMCW_MTI_OFF, bool h16 = false, bool fast = false,
+                                bool q15 = false) {
+  DopplerFn fn = h16 ? doppler_fn_f16(nc, mti, fast) : doppler_fn_f32(nc, mti, fast, q15);
+  switch (nc) {
+#define D_(N) case N: return {fn, DopplerGeom<N>::WR, DopplerGeom<N>::NT};
+    D_(32) D_(64) D_(128) D_(256) D_(512) D_(1024)
+#undef D_
+  }
+  return {nullptr, 0, 0};
+}
+
+// ---- stand-alone 1-D CFAR (fmcw_cfar) and K3 2-D CFAR ---------------------------------------
+using Cfar1Fn = void (*)(const float*, int, int, int, int, Cfar1DArgs, DetSink);
+Cfar1Fn cfar1_fn(uint32_t nc);  // inst_doppler.hip
+using Cfar2Fn = void (*)(const float*, int, int, int, int, int, Cfar2DArgs, DetSink);
+struct Cfar2Info {
+  Cfar2Fn fn;
+  int TR;
+};
+Cfar2Info cfar2_info(uint32_t nc, int hd, int gd);  // inst_cfar2.hip
+size_t cfar2_smem(uint32_t nc, int hr);
+
+}  // namespace fmcw

@@ -188,7 +188,7 @@ __device__ __forceinline__ float2 twiddle(int e) {
 // of at most log2(R) of them (<= 4 roundings), so a group holds log2(R) complex values.
 template <int R, int LR>
 struct GroupTwiddles {
-  static constexpr int NB = R == 2 ? 1 : R == 4 ? 2 : R == 8 ? 3 : 4;
+  static constexpr int NB = R == 2 ? 1 : R == 4 ? 2 : R == 8 ? 3 : R == 16 ? 4 : 5;
   float2 b[NB];
   __device__ __forceinline__ void init(int k) {
 #pragma unroll
@@ -286,6 +286,41 @@ template <> struct Dft<16> {
       for (int k2 = 0; k2 < 4; ++k2) t[k1 + 4 * k2] = v[4 * k1 + k2];
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = t[i];
+  }
+};
+
+template <> struct Dft<32> {
+  __device__ __forceinline__ static void run(float2* v) {
+    // DIT: E = DFT16(even), O = DFT16(odd), X[k] = E[k] + w32^k O[k], X[k+16] = E[k] - w32^k O[k]
+    float2 e[16], o[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      e[i] = v[2 * i];
+      o[i] = v[2 * i + 1];
+    }
+    Dft<16>::run(e);
+    Dft<16>::run(o);
+    const float c8 = 0.70710678118654752440f;
+    // w32^k = (cos(2 pi k / 32), -sin(2 pi k / 32)), k = 1..15 (k = 4, 8, 12 folded below)
+    constexpr float C[16] = {1.f, 0.98078528040323044913f, 0.92387953251128675613f, 0.83146961230254523708f,
+                             0.70710678118654752440f, 0.55557023301960222474f, 0.38268343236508977173f,
+                             0.19509032201612826785f, 0.f, -0.19509032201612826785f, -0.38268343236508977173f,
+                             -0.55557023301960222474f, -0.70710678118654752440f, -0.83146961230254523708f,
+                             -0.92387953251128675613f, -0.98078528040323044913f};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      float2 t;
+      if (k == 0) t = o[0];
+      else if (k == 4) t = cscale(cadd_negi(o[4], o[4]), c8);      // c8 (1 - i) o
+      else if (k == 12) t = cscale(csub_negi(o[12], o[12]), -c8);  // -c8 (1 + i) o
+      else if (k == 8) {                                           // -i o, folded
+        v[8] = cadd_negi(e[8], o[8]);
+        v[24] = csub_negi(e[8], o[8]);
+        continue;
+      } else t = cmul(o[k], make_float2(C[k], k < 8 ? C[k + 8] : -C[k - 8]));  // -sin = cos(. + pi/2)
+      v[k] = cadd(e[k], t);
+      v[k + 16] = csub(e[k], t);
+    }
   }
 };
 
@@ -440,6 +475,72 @@ __device__ __forceinline__ void stockham_to_regs(float2* buf, int t, float2 (*ou
       for (int m = 1; m < R; ++m) out[g][m] = cmul(out[g][m], tw.pow(m));
       Dft<R>::run(out[g]);
     }
+  }
+}
+
+// ---- V values per thread (V = 16 or 32): the passes of the sequential-pair range kernel -------
+// One Stockham radix-R pass in place on `buf` (padded), G = V / R groups j = t + P g per thread,
+// workgroup barriers around the exchange.
+template <int N, int R, int L, int P, int V>
+__device__ __forceinline__ void vpass(float2* buf, int t) {
+  constexpr int G = V / R, S = N / R;
+  static_assert(G * R == V && P * V == N && S % 16 == 0, "V values per thread, immediate read offsets");
+  float2 v[G][R];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const float2* src = buf + pad16(t + P * g);
+#pragma unroll
+    for (int m = 0; m < R; ++m) v[g][m] = src[padoff(m * S)];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int j = t + P * g;
+    const int k = j & (L - 1);
+    if constexpr (L > 1) {
+      GroupTwiddles<R, L * R> tw;
+      tw.init(k);
+#pragma unroll
+      for (int m = 1; m < R; ++m) v[g][m] = cmul(v[g][m], tw.pow(m));
+    }
+    Dft<R>::run(v[g]);
+    float2* dst = buf + pad16((j / L) * L * R + k);
+#pragma unroll
+    for (int m = 0; m < R; ++m) dst[padoff(m * L)] = v[g][m];
+  }
+  __syncthreads();
+}
+
+// Radix-16 passes from sub-transform size L while more than V points remain per transform.
+template <int N, int L, int P, int V>
+__device__ __forceinline__ void vpasses_mid(float2* buf, int t) {
+  if constexpr (N / L > V) {
+    vpass<N, 16, L, P, V>(buf, t);
+    vpasses_mid<N, L * 16, P, V>(buf, t);
+  }
+}
+// Sub-transform size before the last pass when the LDS passes start at L0.
+template <int N, int L0, int V> constexpr int vlast_L() {
+  int L = L0;
+  while (N / L > V) L *= 16;
+  return L;
+}
+// The last pass, into registers: out[g][m] = X[j + m L] for j = t + P g (no barrier after it).
+template <int N, int L, int P, int V>
+__device__ __forceinline__ void vpass_last(const float2* buf, int t, float2 (*out)[N / L]) {
+  constexpr int R = N / L, G = V / R, S = N / R;
+  static_assert(G * R == V && S == L, "last pass: one group per output column");
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int j = t + P * g;
+    const float2* src = buf + pad16(j);
+#pragma unroll
+    for (int m = 0; m < R; ++m) out[g][m] = src[padoff(m * S)];
+    GroupTwiddles<R, N> tw;
+    tw.init(j & (L - 1));
+#pragma unroll
+    for (int m = 1; m < R; ++m) out[g][m] = cmul(out[g][m], tw.pow(m));
+    Dft<R>::run(out[g]);
   }
 }
 

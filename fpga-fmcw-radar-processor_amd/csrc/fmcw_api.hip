@@ -16,9 +16,113 @@
 #include <vector>
 
 #include "../../include/fmcw.h"
-#include "kernels.hpp"
+#include "dispatch.hpp"
 
 using namespace fmcw;
+
+// The host side's own small kernels (one translation unit: no instantiation tables).
+namespace fmcw {
+// --------------------------------------------------------------------------------------
+// Detection ordering: exclusive scan over per-workgroup counts (in workgroup = (frame,
+// range) order), then copy each workgroup's run to its final place.
+// --------------------------------------------------------------------------------------
+// level 1: per 1024-entry block, exclusive scan -> wg_off (block-local) + block sums
+__global__ void __launch_bounds__(1024)
+k_det_scan_blocks(const uint32_t* __restrict__ wg_count, uint32_t* __restrict__ wg_off, int n,
+                  uint32_t* __restrict__ block_sum) {
+  __shared__ int s_wave[1024 / 64 + 2];
+  const int i = blockIdx.x * 1024 + threadIdx.x;
+  const int v = i < n ? (int)wg_count[i] : 0;
+  int total;
+  const int e = block_excl_scan<1024>(v, s_wave, total);
+  if (i < n) wg_off[i] = (uint32_t)e;
+  if (threadIdx.x == 0) block_sum[blockIdx.x] = (uint32_t)total;
+}
+
+// level 2: one workgroup scans the block sums in place (-> block offsets) and the total
+__global__ void __launch_bounds__(1024)
+k_det_scan_top(uint32_t* __restrict__ block_sum, int nb, uint32_t* __restrict__ n_dets,
+               const uint32_t* __restrict__ dropped) {
+  __shared__ int s_wave[1024 / 64 + 2];
+  const int per = (nb + 1023) / 1024;
+  const int b = threadIdx.x * per;
+  const int e = min(b + per, nb);
+  uint32_t s = 0;
+  for (int i = b; i < e; ++i) s += block_sum[i];
+  int total;
+  uint32_t run = (uint32_t)block_excl_scan<1024>((int)s, s_wave, total);
+  for (int i = b; i < e; ++i) {
+    const uint32_t c = block_sum[i];
+    block_sum[i] = run;
+    run += c;
+  }
+  if (threadIdx.x == 0) {
+    n_dets[0] = (uint32_t)total;  // every detection found
+    n_dets[1] = *dropped;         // of which not stored (handle scratch exhausted)
+  }
+}
+
+// One lane per tile; a tile with more than 8 detections (a target's row) is copied by the
+// whole wave, 64 records per step, so one hot tile does not serialise the kernel.
+__global__ void k_det_copy(const fmcw_det* __restrict__ scratch, uint32_t scratch_cap,
+                           const uint32_t* __restrict__ wg_base, const uint32_t* __restrict__ wg_count,
+                           const uint32_t* __restrict__ wg_off, const uint32_t* __restrict__ block_off,
+                           int n, fmcw_det* __restrict__ out, uint32_t cap) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  uint32_t c = 0, b = 0, o = 0;
+  if (i < n) {
+    c = wg_count[i];
+    if (c) {
+      b = wg_base[i];
+      o = block_off[i >> 10] + wg_off[i];
+    }
+  }
+  if (c <= 8)
+    for (uint32_t k = 0; k < c; ++k)
+      if (b + k < scratch_cap && o + k < cap) out[o + k] = scratch[b + k];
+  uint64_t big = __ballot(c > 8);
+  while (big) {
+    const int l = __builtin_ctzll(big);
+    big &= big - 1;
+    const uint32_t cl = (uint32_t)__shfl((int)c, l, 64), bl = (uint32_t)__shfl((int)b, l, 64);
+    const uint32_t ol = (uint32_t)__shfl((int)o, l, 64);
+    for (uint32_t k = lane; k < cl; k += 64)
+      if (bl + k < scratch_cap && ol + k < cap) out[ol + k] = scratch[bl + k];
+  }
+}
+
+// --------------------------------------------------------------------------------------
+// Kernels of the stage entry points.
+// --------------------------------------------------------------------------------------
+// inter (tiled) -> spec[fr][r][c] canonical corner-turner order.
+__global__ void k_unblock(const float2* __restrict__ inter, float2* __restrict__ spec, int ns, int nc,
+                          int T, int RB, size_t total) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const size_t per = (size_t)ns * nc;
+  const size_t fr = i / per;
+  const int rem = (int)(i - fr * per);
+  const int r = rem / nc, c = rem - r * nc;
+  const int ncb = nc / T;
+  const size_t off = ((size_t)((r / RB) * ncb + c / T) * RB + (r % RB)) * T + (c % T);
+  spec[i] = inter[fr * per + off];
+}
+
+__global__ void k_magnitude(const float2* __restrict__ iq, float* __restrict__ out, size_t n, int mode) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float2 X = iq[i];
+  if (mode == FMCW_MAG_AMBM) {
+    const float ai = fabsf(X.x), aq = fabsf(X.y);
+    const float mx = fmaxf(ai, aq), mn = fminf(ai, aq);
+    out[i] = mx + floorf(mn * 0.25f) + floorf(mn * 0.125f);
+  } else {
+    out[i] = mag_sqrt(X.x * X.x + X.y * X.y);
+  }
+}
+
+}  // namespace fmcw
 
 namespace {
 
@@ -58,7 +162,8 @@ struct fmcw_handle {
   int n_cu = 256;
   // range kernel geometry (runtime copies of RangeGeom<N>)
   int T = 0, RB = 0, lgT = 0, lgRB = 0;
-  bool k1_dual = true;     // K1 may use the dual-chirp kernel (fixed at fmcw_create)
+  int k1_want = kRangeSeq;  // preferred K1 family (environment FMCW_K1 at fmcw_create)
+  int k1_kind = kRangeSingle;  // the family the handle runs
   bool k2_fast = false;    // K2 runs its FAST instantiation (fixed at fmcw_create)
   uint32_t chunk = 1;
   // device buffers
@@ -87,28 +192,9 @@ struct fmcw_handle {
   // grid sizes
   int grid_range = 0, grid_doppler = 0, grid_cfar = 0;
   size_t cfar2d_smem = 0;
-  // two-stream chunk pipeline (K1 of chunk c + 1 beside K2 of chunk c, fmcw_enqueue)
-  int pipe_nb = 0;                      // intermediate buffers in the ring (0 = serial chunks)
   size_t inter_bytes = 0;               // h->inter (chunk frames of the K1 -> K2 spectrum)
   int cfar2_steps = 0;                  // 2-D CFAR steps per strip (0 = cost model; FMCW_CFAR2D_STEPS)
-  float2* inter_b[3] = {nullptr, nullptr, nullptr};
-  float* lin_b[3] = {nullptr, nullptr, nullptr};
-  hipStream_t ps[2] = {nullptr, nullptr};
-  hipEvent_t ev_k1[3] = {}, ev_free[3] = {}, ev_fork = nullptr, ev_join = nullptr;
-  // fused K1 + K2 (fused.hpp)
-  bool fused_ok = false;
-  void (*fused_fn)(FusedArgs) = nullptr;
-  int fused_per_xcd = 0, fused_na = 0, fused_nb = 0;
-  float2* fused_spec = nullptr;  // 8 frame spectra, one per XCD (L2-resident)
-  uint32_t* fused_ctl = nullptr;
-  uint64_t* fused_trace = nullptr;  // FMCW_FUSED_TRACE=1: phase timestamps of every launch
-  int64_t fused_fallbacks = 0;
-  bool fused_used_last = false;  // the last fmcw_enqueue ran the fused kernel
-  // paired K1 + K2 launches (pair.hpp): chunk c's range stage beside chunk c - 1's Doppler stage
-  void (*pair_fn)(PairArgs) = nullptr;
-  uint32_t pair_chunk = 0;       // frames per chunk; two chunk spectra (h->inter, pair_b) in flight
-  float2* pair_b = nullptr;
-  int grid_pair = 0;
+  uint32_t last_status[2] = {0, 0};     // fmcw_process: status words 2, 3 of its last call
   // profiling
   bool profiling = false;
   std::vector<PendingEvent> pending;
@@ -119,158 +205,14 @@ struct fmcw_handle {
 
 namespace {
 
-// ---- kernel dispatch tables ------------------------------------------------------------
-using RangeFn = void (*)(const void*, float2*, const float*, const float*, int, int, float);
-
-template <int N, bool H16>
-RangeFn range_fn_t(int dtype, bool q15) {
-  switch (dtype) {
-    case FMCW_IN_F32: return k_range<N, LoadF32, false, H16>;
-    case FMCW_IN_F16: return k_range<N, LoadF16, false, H16>;
-    case FMCW_IN_I16: return q15 ? k_range<N, LoadI16, true, H16> : k_range<N, LoadI16, false, H16>;
-  }
-  return nullptr;
-}
-template <int N>
-RangeFn range_fn(int dtype, bool q15, bool h16) {
-  return h16 ? range_fn_t<N, true>(dtype, q15) : range_fn_t<N, false>(dtype, q15);
-}
-
-struct RangeInfo {
-  RangeFn fn;
-  int T, RB, NT;
-};
-
-template <int N>
-RangeFn range2_fn(int dtype) {
-  if constexpr (RangeGeom<N>::T == 2 && RangeGeom<N>::P >= 128) {
-    switch (dtype) {
-      case FMCW_IN_F32: return k_range2<N, LoadF32>;
-      case FMCW_IN_F16: return k_range2<N, LoadF16>;
-      case FMCW_IN_I16: return k_range2<N, LoadI16>;
-    }
-  }
-  return nullptr;
-}
-
-RangeInfo range_info(uint32_t n, int dtype, int window = FMCW_WIN_HAMMING, bool h16 = false, bool dual = true) {
-  const bool q15 = window == FMCW_WIN_Q15_RTL;
-  // the dual range kernel (kernels.hpp k_range2): T = 2 geometries from FMCW_K1_DUAL up, fp32
-  // window, fp32 spectrum; one thread per (16 points of both chirps).  `dual` = the handle's
-  // choice at fmcw_create (environment FMCW_K1_SINGLE=1 turns it off for A/B runs)
-  if (FMCW_K1_DUAL && dual && n >= (uint32_t)FMCW_K1_DUAL && !q15 && !h16) {
-    switch (n) {
-#define R2_(N) case N: if (RangeFn f = range2_fn<N>(dtype)) return {f, RangeGeom<N>::T, RangeGeom<N>::RB, RangeGeom<N>::P}; break;
-      R2_(2048) R2_(4096) R2_(8192)
-#undef R2_
-    }
-  }
-  switch (n) {
-#define R_(N) case N: return {range_fn<N>(dtype, q15, h16), RangeGeom<N>::T, RangeGeom<N>::RB, RangeGeom<N>::NT};
-    R_(64) R_(128) R_(256) R_(512) R_(1024) R_(2048) R_(4096) R_(8192)
-#undef R_
-  }
-  return {nullptr, 0, 0, 0};
-}
-
-using DopplerFn = void (*)(const float2*, const float*, int, int, int, int, int, int, int, float*,
-                           float*, int, int, Cfar1DArgs, DetSink);
-struct DopplerInfo {
-  DopplerFn fn;
-  int WR, NT;  // range rows per wave tile, threads per workgroup (DopplerGeom::WPB tiles)
-};
-template <int N, bool H16>
-DopplerFn doppler_fn_t(int mti, bool fast) {
-  return mti == FMCW_MTI_2PULSE   ? k_doppler<N, 2, H16>
-         : mti == FMCW_MTI_3PULSE ? k_doppler<N, 3, H16>
-         : fast                   ? k_doppler<N, 0, H16, true>
-                                  : k_doppler<N, 0, H16>;
-}
-template <int N>
-DopplerFn doppler_fn(int mti, bool h16, bool fast) {
-  return h16 ? doppler_fn_t<N, true>(mti, fast) : doppler_fn_t<N, false>(mti, fast);
-}
-// K2's FAST instantiation (kernels.hpp): MTI off, |X| magnitude, no dB map, and the 1-D CFAR
-// (if any) at the reference geometry in fp32
+// K2's FAST instantiation (kernels.hpp): MTI off, |X| magnitude, no dB map, fp32 windows, and the
+// 1-D CFAR (if any) at the reference geometry in fp32
 bool k2_fast(const fmcw_config& c) {
   const bool cfar_ok = c.cfar_kind != FMCW_CFAR_OS1D ||
                        (c.cfar1d_ref == 8 && c.cfar1d_guard == 2 && (int)(2 * c.cfar1d_ref) - (int)c.cfar1d_rank <= 4 &&
                         !(c.compat_rtl & FMCW_COMPAT_CFAR));
-  return c.mti_mode == FMCW_MTI_OFF && c.mag_mode != FMCW_MAG_AMBM && c.map_kind != FMCW_MAP_DB && cfar_ok &&
-         !std::getenv("FMCW_K2_GENERIC");
-}
-DopplerInfo doppler_info(uint32_t nc, int mti = FMCW_MTI_OFF, bool h16 = false, bool fast = false) {
-  switch (nc) {
-#define D_(N) case N: return {doppler_fn<N>(mti, h16, fast), DopplerGeom<N>::WR, DopplerGeom<N>::NT};
-    D_(32) D_(64) D_(128) D_(256) D_(512) D_(1024)
-#undef D_
-  }
-  return {nullptr, 0, 0};
-}
-
-using Cfar1Fn = void (*)(const float*, int, int, int, int, Cfar1DArgs, DetSink);
-Cfar1Fn cfar1_fn(uint32_t nc) {
-  switch (nc) {
-#define C_(N) case N: return k_cfar1d<N>;
-    C_(32) C_(64) C_(128) C_(256) C_(512) C_(1024)
-#undef C_
-  }
-  return nullptr;
-}
-
-using Cfar2Fn = void (*)(const float*, int, int, int, int, int, Cfar2DArgs, DetSink);
-struct Cfar2Info {
-  Cfar2Fn fn;
-  int TR;
-};
-// the reference window (Doppler half extent 6, guard 2: os_cfar_2d as instantiated at
-// radar_core.vhd:376-382) gets the compile-time phase A; any other geometry the generic one
-template <int N>
-Cfar2Fn cfar2_fn(int hd, int gd) {
-  return (hd == 6 && gd == 2) ? k_cfar2d<N, 6, 2> : k_cfar2d<N, 0, 0>;
-}
-Cfar2Info cfar2_info(uint32_t nc, int hd = 0, int gd = 0) {
-  switch (nc) {
-#define C_(N) case N: return {cfar2_fn<N>(hd, gd), Cfar2DGeom<N>::TR};
-    C_(32) C_(64) C_(128) C_(256) C_(512) C_(1024)
-#undef C_
-  }
-  return {nullptr, 0};
-}
-
-// fused K1 + K2 instantiations: the reference core (1024 x 128), BASELINE config 2 (1024 x 256)
-// and two more shapes with 256-thread range and Doppler workgroups and <= 2 MiB spectra
-using FusedFn = void (*)(FusedArgs);
-template <int N, int NC>
-FusedFn fused_fn_t(int dtype) {
-  switch (dtype) {
-    case FMCW_IN_F32: return k_fused<N, NC, LoadF32>;
-    case FMCW_IN_F16: return k_fused<N, NC, LoadF16>;
-    case FMCW_IN_I16: return k_fused<N, NC, LoadI16>;
-  }
-  return nullptr;
-}
-struct FusedInfo {
-  FusedFn fn;
-  int upf, wtpf;
-};
-FusedInfo fused_info(uint32_t n, uint32_t nc, int dtype) {
-#define F_(N, NC) \
-  if (n == N && nc == NC) return {fused_fn_t<N, NC>(dtype), FusedGeom<N, NC>::UPF, FusedGeom<N, NC>::WTPF};
-  F_(1024, 256) F_(1024, 128) F_(512, 256) F_(2048, 128)
-#undef F_
-  return {nullptr, 0, 0};
-}
-
-// paired K1 + K2 instantiations: BASELINE config 2 (1024 x 256)
-using PairFn = void (*)(PairArgs);
-PairFn pair_fn(uint32_t n, uint32_t nc, int dtype) {
-  if (n == 1024 && nc == 256) switch (dtype) {
-      case FMCW_IN_F32: return k_pair<1024, 256, LoadF32>;
-      case FMCW_IN_F16: return k_pair<1024, 256, LoadF16>;
-      case FMCW_IN_I16: return k_pair<1024, 256, LoadI16>;
-    }
-  return nullptr;
+  return c.mti_mode == FMCW_MTI_OFF && c.mag_mode != FMCW_MAG_AMBM && c.map_kind != FMCW_MAP_DB &&
+         c.window != FMCW_WIN_Q15_RTL && cfar_ok && !std::getenv("FMCW_K2_GENERIC");
 }
 
 // 2-D CFAR derived parameters
@@ -303,18 +245,6 @@ Cfar1DArgs cfar1_args(const fmcw_config& c) {
   return a;
 }
 
-size_t cfar2_smem(uint32_t nc, int hr) {
-  switch (nc) {
-    case 32: return cfar2d_smem_bytes<32>(hr);
-    case 64: return cfar2d_smem_bytes<64>(hr);
-    case 128: return cfar2d_smem_bytes<128>(hr);
-    case 256: return cfar2d_smem_bytes<256>(hr);
-    case 512: return cfar2d_smem_bytes<512>(hr);
-    case 1024: return cfar2d_smem_bytes<1024>(hr);
-  }
-  return 0;
-}
-
 int validate(const fmcw_config& c) {
   if (!pow2(c.n_range) || c.n_range < 64 || c.n_range > 8192)
     return fail(FMCW_EINVAL, "n_range=%u: must be a power of two in [64, 8192]", c.n_range);
@@ -335,7 +265,7 @@ int validate(const fmcw_config& c) {
     return fail(FMCW_EINVAL, "map_kind=%d unknown", c.map_kind);
   if (c.mti_mode != FMCW_MTI_OFF && c.mti_mode != FMCW_MTI_2PULSE && c.mti_mode != FMCW_MTI_3PULSE)
     return fail(FMCW_EINVAL, "mti_mode=%d unknown (0 off, 2 or 3 pulse)", c.mti_mode);
-  if (range_info(c.n_range, c.in_dtype).T > (int)c.n_doppler)
+  if (range_info(c.n_range, c.in_dtype, c.window, false, kRangeSeq).T > (int)c.n_doppler)
     return fail(FMCW_EINVAL, "n_doppler=%u smaller than the range kernel's chirp group", c.n_doppler);
   if (c.max_frames < 1) return fail(FMCW_EINVAL, "max_frames must be >= 1");
   if (c.cfar_kind == FMCW_CFAR_OS1D) {
@@ -525,8 +455,7 @@ int launch_det_finish(fmcw_handle* h, size_t n_frames, fmcw_det* dets, size_t de
   ProfScope ps(h, FMCW_K_COMPACT, s);
   hipLaunchKernelGGL(k_det_scan_blocks, dim3(nb), dim3(1024), 0, s, h->wg_count, h->wg_off, n, h->block_sum);
   hipLaunchKernelGGL(k_det_scan_top, dim3(1), dim3(1024), 0, s, h->block_sum, nb, n_dets_dev,
-                     (const uint32_t*)(h->counter + 1),
-                     (const uint32_t*)(h->fused_used_last ? h->fused_ctl + FusedCtl::kErr : nullptr));
+                     (const uint32_t*)(h->counter + 1));
   int rc = check_launch("k_det_scan");
   if (rc) return rc;
   if (dets && det_cap) {
@@ -576,103 +505,6 @@ int ensure_stage(T** p, size_t* have, size_t need_bytes, const char* what) {
 }
 
 }  // namespace
-
-// Decide whether this handle runs the fused K1 + K2 kernel and, if so, verify on the device
-// that its persistent grid lands as the kernel needs: exactly per_xcd workgroups on every XCD,
-// all co-resident (a census launch of the kernel itself: join, wait for the group, exit).
-// Placement is never assumed -- a device or runtime that places differently keeps K1 + K2.
-void setup_fused(fmcw_handle* h) {
-  const fmcw_config& c = h->cfg;
-  // opt-in (FMCW_FUSED=1): measured slower than the K1/K2 pipeline at config 2
-  const char* env = std::getenv("FMCW_FUSED");
-  if (!env || env[0] != '1') return;
-  if (c.n_rx != 1 || c.mti_mode != FMCW_MTI_OFF || c.window == FMCW_WIN_Q15_RTL ||
-      c.spectrum_dtype != FMCW_SPEC_F32)
-    return;
-  if (h->n_cu % 8 != 0) return;
-  const FusedInfo fi = fused_info(c.n_range, c.n_doppler, c.in_dtype);
-  if (!fi.fn) return;
-  int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(fi.fn), 256, 0) !=
-          hipSuccess ||
-      occ < 1) {
-    (void)hipGetLastError();
-    return;
-  }
-  occ = std::min(occ, 4);
-  const int per_xcd = occ * h->n_cu / 8;
-  // Doppler workgroups (4 waves, at most one wave tile each per frame): 3/4 of the group by
-  // default (FMCW_FUSED_NB overrides), at least enough to cover a frame's wave tiles
-  const char* nbs = std::getenv("FMCW_FUSED_NB");
-  int nb = nbs ? std::atoi(nbs) : per_xcd * 3 / 4;
-  nb = std::max(nb, (fi.wtpf + 3) / 4);
-  const int na = std::min(per_xcd - nb, fi.upf);  // every range workgroup has a unit per frame
-  if (na < 8) return;
-  const size_t spec_bytes = 8 * kRing * (size_t)c.n_range * c.n_doppler * sizeof(float2);
-  if (hipMalloc(reinterpret_cast<void**>(&h->fused_spec), spec_bytes) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&h->fused_ctl), FusedCtl::kWords * 4) != hipSuccess) {
-    (void)hipGetLastError();
-    return;
-  }
-  FusedArgs a{};
-  a.ctl = h->fused_ctl;
-  a.per_xcd = per_xcd;
-  a.n_a = na;
-  a.n_b = nb;
-  a.census = 1;
-  a.spin_limit = 20000;
-  std::vector<uint32_t> ctl(FusedCtl::kWords, 0);
-  if (hipMemset(h->fused_ctl, 0, FusedCtl::kWords * 4) != hipSuccess) return;
-  hipLaunchKernelGGL(fi.fn, dim3(8 * per_xcd), dim3(256), 0, 0, a);
-  if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
-      hipMemcpy(ctl.data(), h->fused_ctl, FusedCtl::kWords * 4, hipMemcpyDeviceToHost) != hipSuccess) {
-    (void)hipGetLastError();
-    return;
-  }
-  if (ctl[FusedCtl::kErr] != 0) return;
-  for (int x = 0; x < 8; ++x)
-    if (ctl[FusedCtl::join(x)] != (uint32_t)per_xcd) return;
-  if (std::getenv("FMCW_FUSED_VERBOSE"))
-    std::fprintf(stderr, "fmcw: fused kernel on, %d workgroups per XCD (%d range, %d Doppler)\n", per_xcd, na, nb);
-  const char* tr = std::getenv("FMCW_FUSED_TRACE");
-  if (tr && tr[0] == '1' && hipMalloc(reinterpret_cast<void**>(&h->fused_trace), 8 * kTraceFrames * 8 * 8) != hipSuccess) {
-    (void)hipGetLastError();
-    h->fused_trace = nullptr;
-  }
-  h->fused_fn = fi.fn;
-  h->fused_per_xcd = per_xcd;
-  h->fused_na = na;
-  h->fused_nb = nb;
-  h->fused_ok = true;
-}
-
-// Paired launches (pair.hpp), default on where instantiated: one rx, MTI off, the FAST K2
-// configuration without the 2-D CFAR, fp32 window and spectrum.  Chunk: the largest multiple of
-// the frames one round of the persistent grid covers with both chunk spectra (written and read)
-// within ~3/4 of the 256 MiB Infinity Cache.  FMCW_PAIR=0 / 1 overrides kPairDefault (A/B runs).
-constexpr bool kPairDefault = false;
-void setup_pair(fmcw_handle* h, size_t frame_inter) {
-  const fmcw_config& c = h->cfg;
-  const char* env = std::getenv("FMCW_PAIR");
-  if (!(env ? env[0] == '1' : kPairDefault)) return;
-  if (c.n_rx != 1 || c.window == FMCW_WIN_Q15_RTL || c.spectrum_dtype != FMCW_SPEC_F32 ||
-      c.cfar_kind == FMCW_CFAR_OS2D || !h->k2_fast)
-    return;
-  const PairFn fn = pair_fn(c.n_range, c.n_doppler, c.in_dtype);
-  if (!fn) return;
-  occupancy_grid(fn, 256, 0, h->n_cu, &h->grid_pair);
-  const size_t tpf = (size_t)c.n_range / doppler_info(c.n_doppler).WR;
-  const size_t units_pf = tpf / kWavesPerBlock;  // K2 items per frame (K1: n_doppler / T)
-  size_t ch = std::max<size_t>(1, (192u << 20) / (2 * frame_inter));
-  if ((size_t)h->grid_pair % units_pf == 0) {
-    const size_t unit = (size_t)h->grid_pair / units_pf;
-    if (ch >= 2 * unit) ch -= ch % unit;
-  }
-  if (const char* pc = std::getenv("FMCW_PAIR_CHUNK")) ch = (size_t)std::max(1, std::atoi(pc));
-  h->pair_chunk = (uint32_t)std::min<size_t>(ch, c.max_frames);
-  if (h->pair_chunk >= c.max_frames) return;  // a batch never spans two chunks: nothing to pair
-  h->pair_fn = fn;
-}
 
 // the thread-local fmcw_last_error() message, for the other translation units of the library
 int fmcw_internal_fail(int code, const char* msg) { return fail(code, "%s", msg); }
@@ -755,9 +587,13 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   h->cfg = *cfg;
   const fmcw_config& c = h->cfg;
   h->n_cu = prop.multiProcessorCount;
-  h->k1_dual = !std::getenv("FMCW_K1_SINGLE");
+  // K1 family: the sequential-pair kernel where instantiated (N = 4096, 8192), else the dual
+  // one (N >= 2048), else k_range; environment FMCW_K1=single|dual|seq caps it (A/B runs)
+  if (const char* k1 = std::getenv("FMCW_K1"))
+    h->k1_want = !std::strcmp(k1, "single") ? kRangeSingle : !std::strcmp(k1, "dual") ? kRangeDual : kRangeSeq;
   h->k2_fast = k2_fast(c);
-  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, c.spectrum_dtype == FMCW_SPEC_F16, h->k1_dual);
+  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, c.spectrum_dtype == FMCW_SPEC_F16, h->k1_want);
+  h->k1_kind = ri.kind;
   h->T = ri.T;
   h->RB = ri.RB;
   h->lgT = __builtin_ctz(ri.T);
@@ -765,27 +601,10 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   const size_t frame_inter = (size_t)c.n_rx * c.n_range * c.n_doppler *
                              (c.spectrum_dtype == FMCW_SPEC_F16 ? sizeof(uint32_t) : sizeof(float2));
   occupancy_grid(ri.fn, ri.NT, 0, h->n_cu, &h->grid_range);
-#ifdef FMCW_K1_GRID_PER_CU  // tuning switch (tools/build_variants.sh): K1 workgroups per CU
-  h->grid_range = std::min(h->grid_range, FMCW_K1_GRID_PER_CU * h->n_cu);
-#endif
   const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype == FMCW_SPEC_F16, h->k2_fast);
   occupancy_grid(di.fn, di.NT, 0, h->n_cu, &h->grid_doppler);
-  // two-stream pipeline of chunks (FMCW_PIPE=1): ring of FMCW_PIPE_BUFS intermediate buffers of
-  // FMCW_PIPE_CHUNK frames, sized so the ring stays in the 256 MiB Infinity Cache
   if (const char* cs = std::getenv("FMCW_CFAR2D_STEPS")) h->cfar2_steps = std::max(0, std::atoi(cs));
-  const char* pe = std::getenv("FMCW_PIPE");
-  const bool pipe = pe && pe[0] == '1';
-  if (pipe) {
-    const char* pc = std::getenv("FMCW_PIPE_CHUNK");
-    const char* pb = std::getenv("FMCW_PIPE_BUFS");
-    h->pipe_nb = std::max(2, std::min(3, pb ? std::atoi(pb) : 2));
-    const size_t want = pc ? (size_t)std::max(1, std::atoi(pc)) : std::max<size_t>(1, (64u << 20) / frame_inter);
-    h->chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(c.max_frames, want));
-  } else if (c.chunk_frames) {
-    h->chunk = std::min<uint32_t>(c.chunk_frames, c.max_frames);
-  } else {
-    h->chunk = auto_chunk(h, frame_inter);
-  }
+  h->chunk = c.chunk_frames ? std::min<uint32_t>(c.chunk_frames, c.max_frames) : auto_chunk(h, frame_inter);
   auto cleanup = [&](int code) {
     fmcw_destroy(h);
     return code;
@@ -799,33 +618,12 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   } while (0)
   ALLOC(h->win_r, c.n_range * sizeof(float));
   ALLOC(h->win_d, c.n_doppler * sizeof(float));
-  // >= one fp32 frame: fmcw_range_ct writes the fp32 spectrum through it whatever spectrum_dtype
-  setup_pair(h, frame_inter);
-  // K1 addresses a launch's spectrum with 32-bit byte offsets (write-through buffer stores)
+  // K1 / K2 address a launch's spectrum with 32-bit byte offsets (buffer loads and stores)
   h->chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(h->chunk, ((size_t)1 << 32) / frame_inter - 1));
-  h->inter_bytes = std::max(std::max<size_t>(h->chunk, h->pair_fn ? h->pair_chunk : 0) * frame_inter,
-                            (size_t)c.n_rx * c.n_range * c.n_doppler * sizeof(float2));
+  // >= one fp32 frame: fmcw_range_ct writes the fp32 spectrum through it whatever spectrum_dtype
+  h->inter_bytes = std::max((size_t)h->chunk * frame_inter, (size_t)c.n_rx * c.n_range * c.n_doppler * sizeof(float2));
   ALLOC(h->inter, h->inter_bytes);
-  if (h->pair_fn) ALLOC(h->pair_b, (size_t)h->pair_chunk * frame_inter);
   if (c.cfar_kind == FMCW_CFAR_OS2D) ALLOC(h->lin_scratch, (size_t)h->chunk * c.n_range * c.n_doppler * sizeof(float));
-  if (h->pipe_nb) {
-    h->inter_b[0] = h->inter;
-    h->lin_b[0] = h->lin_scratch;
-    for (int b = 1; b < h->pipe_nb; ++b) {
-      ALLOC(h->inter_b[b], h->chunk * frame_inter);
-      if (c.cfar_kind == FMCW_CFAR_OS2D) ALLOC(h->lin_b[b], (size_t)h->chunk * c.n_range * c.n_doppler * sizeof(float));
-    }
-    for (int i = 0; i < 2; ++i)
-      if (hipStreamCreateWithFlags(&h->ps[i], hipStreamNonBlocking) != hipSuccess)
-        return cleanup(fail(FMCW_EHIP, "stream create"));
-    for (int b = 0; b < h->pipe_nb; ++b)
-      if (hipEventCreateWithFlags(&h->ev_k1[b], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&h->ev_free[b], hipEventDisableTiming) != hipSuccess)
-        return cleanup(fail(FMCW_EHIP, "event create"));
-    if (hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess)
-      return cleanup(fail(FMCW_EHIP, "event create"));
-  }
   h->n_wg_max = (size_t)c.max_frames * tiles_per_frame(h);
   {
     // Each tile owns a slot of 1/32 of its cells (a 3 % detection density, far above any
@@ -852,7 +650,7 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   {
     // the range table carries the 2^-range_shift scaling (Q15: applied after the integer window)
     std::vector<float> wr = window_table(c.n_range, c.window, c.window == FMCW_WIN_Q15_RTL ? 0 : c.range_shift),
-                       wd = window_table(c.n_doppler, c.window == FMCW_WIN_Q15_RTL ? FMCW_WIN_HAMMING : c.window);
+                       wd = window_table(c.n_doppler, c.window);  // Q15: the ROM integers, applied by K2
     if (hipMemcpy(h->win_r, wr.data(), wr.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(h->win_d, wd.data(), wd.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(h->wg_count, 0, h->n_wg_max * sizeof(uint32_t)) != hipSuccess)
@@ -867,7 +665,6 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
       (void)hipGetLastError();
     occupancy_grid(ci.fn, 256, h->cfar2d_smem, h->n_cu, &h->grid_cfar);
   }
-  setup_fused(h);
   *out = h;
   return FMCW_OK;
 }
@@ -877,8 +674,7 @@ int fmcw_destroy(fmcw_handle* h) {
   hipSetDevice(h->cfg.device_id);
   void* ptrs[] = {h->win_r, h->win_d, h->inter, h->lin_scratch, h->det_scratch, h->counter,
                   h->n_dets_tmp, h->wg_base, h->wg_count, h->wg_off, h->block_sum,
-                  h->stage_cube, h->stage_map, h->stage_dets, h->fused_spec, h->fused_ctl, h->fused_trace,
-                  h->pair_b};
+                  h->stage_cube, h->stage_map, h->stage_dets};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& pe : h->pending) {
@@ -886,18 +682,6 @@ int fmcw_destroy(fmcw_handle* h) {
     hipEventDestroy(pe.b);
   }
   for (auto e : h->free_events) hipEventDestroy(e);
-  for (int b = 1; b < 3; ++b) {
-    if (h->inter_b[b]) hipFree(h->inter_b[b]);
-    if (h->lin_b[b]) hipFree(h->lin_b[b]);
-  }
-  for (int b = 0; b < 3; ++b) {
-    if (h->ev_k1[b]) hipEventDestroy(h->ev_k1[b]);
-    if (h->ev_free[b]) hipEventDestroy(h->ev_free[b]);
-  }
-  if (h->ev_fork) hipEventDestroy(h->ev_fork);
-  if (h->ev_join) hipEventDestroy(h->ev_join);
-  for (int i = 0; i < 2; ++i)
-    if (h->ps[i]) hipStreamDestroy(h->ps[i]);
   delete h;
   return FMCW_OK;
 }
@@ -912,158 +696,61 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
     return fail(FMCW_EINVAL, "n_dets_dev is required when a CFAR is configured");
   HIP_TRY(hipSetDevice(c.device_id));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, c.spectrum_dtype == FMCW_SPEC_F16, h->k1_dual);
+  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, c.spectrum_dtype == FMCW_SPEC_F16, h->k1_want);
   const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype == FMCW_SPEC_F16, h->k2_fast);
   const size_t frame_px = (size_t)c.n_range * c.n_doppler;
   const size_t in_frame_bytes = cube_bytes(c, 1);
   const Cfar1DArgs cf1 = cfar1_args(c);
-  const DetSink sink = make_sink(h);
+  const bool q15 = c.window == FMCW_WIN_Q15_RTL;
+  // status words 2 / 3 (saturations) are counted atomically by the kernels that can saturate
+  uint32_t* const status = n_dets_dev ? n_dets_dev + 2 : nullptr;
   int rc;
   if (c.cfar_kind != FMCW_CFAR_NONE) HIP_TRY(hipMemsetAsync(h->counter, 0, 2 * sizeof(uint32_t), s));
+  if (n_dets_dev) HIP_TRY(hipMemsetAsync(n_dets_dev, 0, FMCW_STATUS_WORDS * sizeof(uint32_t), s));
 
-  // fused K1 + K2: one persistent launch for the whole batch (the 2-D CFAR needs the whole
-  // linear map, so it runs on the fused path only when the caller asks for that map)
-  const bool fuse = h->fused_ok && (c.cfar_kind != FMCW_CFAR_OS2D || (rd_map && c.map_kind == FMCW_MAP_LINEAR));
-  h->fused_used_last = fuse;
-  if (fuse) {
-    HIP_TRY(hipMemsetAsync(h->fused_ctl, 0, FusedCtl::kWords * 4, s));
-    FusedArgs a{};
-    a.cube = cube;
-    a.spec = h->fused_spec;
-    a.win_r = h->win_r;
-    a.chirp_w = h->win_d;
-    a.lin_map = rd_map && c.map_kind == FMCW_MAP_LINEAR ? rd_map : nullptr;
-    a.db_map = rd_map && c.map_kind == FMCW_MAP_DB ? rd_map : nullptr;
-    a.ctl = h->fused_ctl;
-    a.n_frames = (int)n_frames;
-    a.frame0 = 0;
-    a.tile0 = 0;
-    a.per_xcd = h->fused_per_xcd;
-    a.n_a = h->fused_na;
-    a.n_b = h->fused_nb;
-    a.mag_mode = c.mag_mode;
-    a.census = 0;
-    a.spin_limit = 2000000;  // ~0.1-1 s of polling: only a broken group ever reaches it
-    a.cf = cf1;
-    a.sink = sink;
-    a.trace = h->fused_trace;
-    if (h->fused_trace) HIP_TRY(hipMemsetAsync(h->fused_trace, 0, 8 * kTraceFrames * 8 * 8, s));
-    {
-      ProfScope ps(h, FMCW_K_FUSED, s);
-      hipLaunchKernelGGL(h->fused_fn, dim3(8 * h->fused_per_xcd), dim3(256), 0, s, a);
-      if ((rc = check_launch("k_fused"))) return rc;
-    }
-    if (c.cfar_kind == FMCW_CFAR_OS2D)
-      for (size_t f0 = 0; f0 < n_frames; f0 += std::max<size_t>(h->chunk, kCfar2Batch)) {
-        const int nf = (int)std::min<size_t>(std::max<size_t>(h->chunk, kCfar2Batch), n_frames - f0);
-        if ((rc = launch_cfar(h, rd_map + f0 * frame_px, nf, (int)f0, s))) return rc;
-      }
-    if (c.cfar_kind != FMCW_CFAR_NONE) return launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, s);
-    return FMCW_OK;
-  }
-
-  // Paired launches: launch i runs K1 of chunk i into buffer i % 2 beside K2 of chunk i - 1
-  // from buffer (i - 1) % 2; the kernel boundary orders every write before its read
-  if (h->pair_fn && n_frames > h->pair_chunk) {
-    const size_t C = h->pair_chunk;
-    const size_t n_chunks = (n_frames + C - 1) / C;
-    const size_t tpf = c.n_range / di.WR;
-    float2* bufs[2] = {h->inter, h->pair_b};
-    for (size_t i = 0; i <= n_chunks; ++i) {
-      PairArgs a{};
-      a.win_r = h->win_r;
-      a.chirp_w = h->win_d;
-      a.cf = cf1;
-      a.sink = sink;
-      if (i < n_chunks) {
-        const size_t f0 = i * C, nf = std::min(C, n_frames - f0);
-        a.cube = static_cast<const char*>(cube) + f0 * in_frame_bytes;
-        a.inter_w = bufs[i & 1];
-        a.n_groups = (int)(nf * (c.n_doppler / ri.T));
-      }
-      if (i >= 1) {
-        const size_t f0 = (i - 1) * C, nf = std::min(C, n_frames - f0);
-        a.inter_r = bufs[(i - 1) & 1];
-        a.n_tiles = (int)(nf * tpf);
-        a.frame0 = (int)f0;
-        a.tile0 = (int)(f0 * tpf);
-        a.lin_map = rd_map && c.map_kind == FMCW_MAP_LINEAR ? rd_map + f0 * frame_px : nullptr;
-      }
-      const int items = std::max(a.n_groups, a.n_tiles / kWavesPerBlock);
-      ProfScope ps(h, FMCW_K_PAIR, s);
-      hipLaunchKernelGGL(h->pair_fn, dim3(std::min(items, h->grid_pair)), dim3(256), 0, s, a);
-      if ((rc = check_launch("k_pair"))) return rc;
-    }
-    if (c.cfar_kind != FMCW_CFAR_NONE) return launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, s);
-    return FMCW_OK;
-  }
-
-  // Chunks of h->chunk frames: K1 -> intermediate -> K2 (+ K3).  With the two-stream pipeline
-  // (h->pipe_nb buffers) chunk c's K1 runs on ps[0] beside chunk c - 1's K2 on ps[1]; buffer b
-  // is rewritten by K1 only after the K2 that read it (ev_free[b]).  Fork from / join to the
-  // caller's stream with events, so the call stays stream-ordered (and graph-capturable).
+  // Chunks of h->chunk frames: K1 -> corner-turned spectrum -> K2 (+ K3)
   const size_t n_chunks = (n_frames + h->chunk - 1) / h->chunk;
-  const bool piped = h->pipe_nb > 0 && n_chunks > 1;
-  hipStream_t sa = s, sb = s;
-  if (piped) {
-    sa = h->ps[0];
-    sb = h->ps[1];
-    HIP_TRY(hipEventRecord(h->ev_fork, s));
-    HIP_TRY(hipStreamWaitEvent(sa, h->ev_fork, 0));
-    HIP_TRY(hipStreamWaitEvent(sb, h->ev_fork, 0));
-  }
   size_t k3_f0 = 0;  // first frame of the caller's map not yet through the 2-D CFAR
   for (size_t ci = 0; ci < n_chunks; ++ci) {
     const size_t f0 = ci * h->chunk;
     const int nf = (int)std::min<size_t>(h->chunk, n_frames - f0);
     const void* src = static_cast<const char*>(cube) + f0 * in_frame_bytes;
-    const int b = piped ? (int)(ci % h->pipe_nb) : 0;
-    float2* inter = piped ? h->inter_b[b] : h->inter;
-    if (piped && ci >= (size_t)h->pipe_nb) HIP_TRY(hipStreamWaitEvent(sa, h->ev_free[b], 0));
     {
       const int n_groups = nf * (int)c.n_rx * (int)(c.n_doppler / ri.T);
-      ProfScope ps(h, FMCW_K_RANGE, sa);
-      // MTI off: K1 applies the Doppler window too (k_doppler<NC, 0> expects it)
-      const float* chirp_w = c.mti_mode == FMCW_MTI_OFF ? h->win_d : nullptr;
-      hipLaunchKernelGGL(ri.fn, dim3(std::min(n_groups, h->grid_range)), dim3(ri.NT), 0, sa, src, inter,
-                         h->win_r, chirp_w, (int)c.n_doppler, n_groups, q15_scale(c));
+      ProfScope ps(h, FMCW_K_RANGE, s);
+      // MTI off, fp32 window: K1 applies the Doppler window too (FFT linearity; K2 then skips
+      // it); with MTI or the RTL-compat integer window K2 applies it after the canceller
+      const float* chirp_w = c.mti_mode == FMCW_MTI_OFF && !q15 ? h->win_d : nullptr;
+      hipLaunchKernelGGL(ri.fn, dim3(std::min(n_groups, h->grid_range)), dim3(ri.NT), 0, s, src, h->inter,
+                         h->win_r, chirp_w, (int)c.n_doppler, n_groups, q15_scale(c), status);
       if ((rc = check_launch("k_range"))) return rc;
-    }
-    if (piped) {
-      HIP_TRY(hipEventRecord(h->ev_k1[b], sa));
-      HIP_TRY(hipStreamWaitEvent(sb, h->ev_k1[b], 0));
     }
     float* lin = nullptr;
     float* db = nullptr;
     if (rd_map && c.map_kind == FMCW_MAP_LINEAR) lin = rd_map + f0 * frame_px;
     if (rd_map && c.map_kind == FMCW_MAP_DB) db = rd_map + f0 * frame_px;
-    if (c.cfar_kind == FMCW_CFAR_OS2D && !lin) lin = piped ? h->lin_b[b] : h->lin_scratch;
+    if (c.cfar_kind == FMCW_CFAR_OS2D && !lin) lin = h->lin_scratch;
     {
       const int n_tiles = nf * (int)(c.n_range / di.WR);
       const int grid = std::min((n_tiles + kWavesPerBlock - 1) / kWavesPerBlock, h->grid_doppler);
-      ProfScope ps(h, FMCW_K_DOPPLER, sb);
-      hipLaunchKernelGGL(di.fn, dim3(grid), dim3(di.NT), 0, sb, inter,
-                         h->win_d, (int)c.n_range, (int)c.n_rx, h->lgT, h->lgRB, n_tiles, (int)f0,
-                         (int)(f0 * (c.n_range / di.WR)), lin, db, c.mag_mode,
-                         (c.compat_rtl & FMCW_COMPAT_MTI) ? 1 : 0, cf1, sink);
+      ProfScope ps(h, FMCW_K_DOPPLER, s);
+      hipLaunchKernelGGL(di.fn, dim3(grid), dim3(di.NT), 0, s, h->inter, h->win_d, (int)c.n_range,
+                         (int)c.n_rx, h->lgT, h->lgRB, n_tiles, (int)f0, (int)(f0 * (c.n_range / di.WR)), lin,
+                         db, c.mag_mode, (c.compat_rtl & FMCW_COMPAT_MTI) ? 1 : 0, q15 ? 1 : 0, cf1,
+                         make_sink(h), status);
       if ((rc = check_launch("k_doppler"))) return rc;
     }
-    if (piped) HIP_TRY(hipEventRecord(h->ev_free[b], sb));
     if (c.cfar_kind == FMCW_CFAR_OS2D) {
       // on the caller's map the 2-D CFAR runs over batches of >= kCfar2Batch frames: its
       // strips then cover more rows per workgroup and more frames share one launch
       const size_t done = f0 + (size_t)nf;
       if (!(rd_map && c.map_kind == FMCW_MAP_LINEAR)) {  // chunk scratch: this chunk only
-        if ((rc = launch_cfar(h, lin, nf, (int)f0, sb))) return rc;
+        if ((rc = launch_cfar(h, lin, nf, (int)f0, s))) return rc;
       } else if (done - k3_f0 >= kCfar2Batch || done == n_frames) {
-        if ((rc = launch_cfar(h, rd_map + k3_f0 * frame_px, (int)(done - k3_f0), (int)k3_f0, sb))) return rc;
+        if ((rc = launch_cfar(h, rd_map + k3_f0 * frame_px, (int)(done - k3_f0), (int)k3_f0, s))) return rc;
         k3_f0 = done;
       }
     }
-  }
-  if (piped) {  // join: everything on ps[0] precedes ps[1]'s last K2, so ps[1] alone is enough
-    HIP_TRY(hipEventRecord(h->ev_join, sb));
-    HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));
   }
   if (c.cfar_kind != FMCW_CFAR_NONE) return launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, s);
   return FMCW_OK;
@@ -1099,24 +786,13 @@ int fmcw_process(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
     d_dets = h->stage_dets;
   }
   if ((rc = fmcw_enqueue(h, d_cube, n_frames, d_map, d_dets, det_cap, h->n_dets_tmp, stream))) return rc;
-  uint32_t ndd[2] = {0, 0};  // found, dropped
-  hipError_t e = hipSuccess;
-  if (c.cfar_kind != FMCW_CFAR_NONE)
-    e = hipMemcpyAsync(ndd, h->n_dets_tmp, sizeof ndd, hipMemcpyDeviceToHost, s);
+  uint32_t ndd[FMCW_STATUS_WORDS] = {0, 0, 0, 0};  // found, dropped, window / word saturations
+  hipError_t e = hipMemcpyAsync(ndd, h->n_dets_tmp, sizeof ndd, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess && rd_map && d_map != rd_map)
     e = hipMemcpyAsync(rd_map, d_map, map_bytes, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e == hipSuccess && h->fused_used_last) {
-    uint32_t ferr = 0;
-    e = hipMemcpy(&ferr, h->fused_ctl + FusedCtl::kErr, 4, hipMemcpyDeviceToHost);
-    if (e == hipSuccess && ferr) {
-      // the fused launch gave up (a bounded wait expired): redo the batch on K1 + K2 and keep
-      // this handle there
-      h->fused_ok = false;
-      h->fused_fallbacks += 1;
-      return fmcw_process(h, cube, n_frames, rd_map, dets, det_cap, n_dets, stream);
-    }
-  }
+  h->last_status[0] = ndd[2];
+  h->last_status[1] = ndd[3];
   const uint32_t nd = ndd[0];
   if (e == hipSuccess && dets && d_dets != dets && nd)
     e = hipMemcpy(dets, d_dets, std::min<size_t>(nd, det_cap) * sizeof(fmcw_det), hipMemcpyDeviceToHost);
@@ -1136,7 +812,7 @@ int fmcw_range_ct(fmcw_handle* h, const void* cube, size_t n_frames, void* spec,
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // the stage output is the fp32 spectrum whatever spectrum_dtype the path uses: K1's fp32
   // variant, as many frames per launch as the intermediate buffer holds at 8 B per point
-  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, false, h->k1_dual);
+  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, false, h->k1_want);
   const size_t in_frame_bytes = cube_bytes(c, 1);
   const size_t fr_px = (size_t)c.n_rx * c.n_range * c.n_doppler;
   const size_t rc_chunk = std::max<size_t>(1, h->inter_bytes / (fr_px * sizeof(float2)));
@@ -1147,7 +823,7 @@ int fmcw_range_ct(fmcw_handle* h, const void* cube, size_t n_frames, void* spec,
       ProfScope ps(h, FMCW_K_RANGE, s);
       hipLaunchKernelGGL(ri.fn, dim3(std::min(n_groups, h->grid_range)), dim3(ri.NT), 0, s,
                          static_cast<const char*>(cube) + f0 * in_frame_bytes, h->inter, h->win_r,
-                         (const float*)nullptr, (int)c.n_doppler, n_groups, q15_scale(c));
+                         (const float*)nullptr, (int)c.n_doppler, n_groups, q15_scale(c), (uint32_t*)nullptr);
       int rc = check_launch("k_range");
       if (rc) return rc;
     }
@@ -1179,8 +855,8 @@ int fmcw_cfar(fmcw_handle* h, const float* map, size_t n_frames, fmcw_det* dets,
   if (n_frames < 1 || n_frames > c.max_frames) return fail(FMCW_EINVAL, "n_frames out of range");
   HIP_TRY(hipSetDevice(c.device_id));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  h->fused_used_last = false;
   HIP_TRY(hipMemsetAsync(h->counter, 0, 2 * sizeof(uint32_t), s));
+  HIP_TRY(hipMemsetAsync(n_dets_dev, 0, FMCW_STATUS_WORDS * sizeof(uint32_t), s));
   int rc = launch_cfar(h, map, (int)n_frames, 0, s);
   if (rc) return rc;
   return launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, s);
@@ -1195,21 +871,12 @@ int fmcw_set_profiling(fmcw_handle* h, int enable) {
 int fmcw_get_info(fmcw_handle* h, int key, int64_t* value) {
   if (!h || !value) return fail(FMCW_EINVAL, "null argument");
   switch (key) {
-    case FMCW_INFO_FUSED: *value = h->fused_ok ? 1 : 0; return FMCW_OK;
-    case FMCW_INFO_FUSED_GROUP: *value = h->fused_per_xcd; return FMCW_OK;
-    case FMCW_INFO_FUSED_FALLBACKS: *value = h->fused_fallbacks; return FMCW_OK;
     case FMCW_INFO_CHUNK: *value = h->chunk; return FMCW_OK;
-    case FMCW_INFO_PAIR_CHUNK: *value = h->pair_fn ? h->pair_chunk : 0; return FMCW_OK;
+    case FMCW_INFO_RANGE_KERNEL: *value = h->k1_kind; return FMCW_OK;
+    case FMCW_INFO_WINDOW_SATURATIONS: *value = h->last_status[0]; return FMCW_OK;
+    case FMCW_INFO_WORD_SATURATIONS: *value = h->last_status[1]; return FMCW_OK;
   }
   return fail(FMCW_EINVAL, "fmcw_get_info: unknown key %d", key);
-}
-
-int fmcw_get_fused_trace(fmcw_handle* h, uint64_t* out, size_t n_words) {
-  if (!h || !out) return fail(FMCW_EINVAL, "null argument");
-  if (!h->fused_trace) return fail(FMCW_EINVAL, "no fused trace (create the handle with FMCW_FUSED_TRACE=1)");
-  HIP_TRY(hipSetDevice(h->cfg.device_id));
-  HIP_TRY(hipMemcpy(out, h->fused_trace, std::min<size_t>(n_words, 8 * kTraceFrames * 8) * 8, hipMemcpyDeviceToHost));
-  return FMCW_OK;
 }
 
 int fmcw_kernel_times(fmcw_handle* h, double* ms, uint64_t* launches) {

@@ -9,6 +9,8 @@
 // ncclSend / ncclRecv / ncclGroupEnd -> compact) and never synchronises with the CPU.
 // At config 4 (1024 frames per GPU, ~64 detections per frame) a 128-per-frame wire_cap is
 // 2 MiB per rank: tens of microseconds on one 64 GB/s xGMI link, beside a 1.4 ms step.
+// wire_cap is part of the communicator (fmcw_comm_create, checked equal on every rank there),
+// so the send and receive sizes always match and the gather allocates nothing.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -32,11 +34,13 @@ int gfail(int code, const char* fmt, ...) {
   return fmcw_internal_fail(code, b);
 }
 
-// rank-local: header + min(n, wire_cap) records with the frame offset applied
-__global__ void k_gather_pack(const fmcw_det* __restrict__ dets, const uint32_t* __restrict__ n_dets,
+// rank-local: header + min(found, det_cap, wire_cap) records with the frame offset applied.
+// n_dets[0] may exceed det_cap (fmcw_enqueue writes at most det_cap records), so the records
+// past det_cap are never read: they count as lost, with the scratch losses n_dets[1].
+__global__ void k_gather_pack(const fmcw_det* __restrict__ dets, uint32_t det_cap, const uint32_t* __restrict__ n_dets,
                               uint32_t wire_cap, uint32_t frame_offset, fmcw_det* __restrict__ wire) {
   const uint32_t found = n_dets[0], lost_scratch = n_dets[1];
-  const uint32_t n = found < wire_cap ? found : wire_cap;
+  const uint32_t n = min(found, min(det_cap, wire_cap));
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) {
     uint32_t* hdr = reinterpret_cast<uint32_t*>(wire);
@@ -61,7 +65,7 @@ __global__ void __launch_bounds__(256) k_gather_compact(const fmcw_det* __restri
   const int tid = threadIdx.x;
   if (tid < 64) {
     const uint32_t* hdr = reinterpret_cast<const uint32_t*>(recv + (size_t)tid * (1 + wire_cap));
-    const uint32_t c = tid < n_ranks ? hdr[0] : 0u, l = tid < n_ranks ? hdr[1] : 0u;
+    const uint32_t c = tid < n_ranks ? min(hdr[0], wire_cap) : 0u, l = tid < n_ranks ? hdr[1] : 0u;
     uint32_t x = c, lx = l;
     for (int d = 1; d < 64; d <<= 1) {
       const uint32_t y = __shfl_up(x, d, 64), ly = __shfl_up(lx, d, 64);
@@ -95,26 +99,8 @@ struct fmcw_comm {
   int n_ranks = 0, rank = 0, device_id = 0;
   fmcw_det* wire = nullptr;   // this rank's outgoing message
   fmcw_det* recv = nullptr;   // root: n_ranks messages
-  size_t wire_cap = 0;        // capacity the buffers are sized for
+  size_t wire_cap = 0;        // record slots per rank message (equal on every rank)
 };
-
-namespace {
-int ensure_wire(fmcw_comm* c, size_t wire_cap) {
-  if (c->wire_cap >= wire_cap && c->wire) return FMCW_OK;
-  if (c->wire) hipFree(c->wire);
-  if (c->recv) hipFree(c->recv);
-  c->wire = c->recv = nullptr;
-  c->wire_cap = 0;
-  const size_t msg = (1 + wire_cap) * sizeof(fmcw_det);
-  if (hipMalloc(reinterpret_cast<void**>(&c->wire), msg) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&c->recv), msg * (size_t)c->n_ranks) != hipSuccess) {
-    (void)hipGetLastError();
-    return gfail(FMCW_ENOMEM, "gather buffers (%zu B per rank) failed", msg);
-  }
-  c->wire_cap = wire_cap;
-  return FMCW_OK;
-}
-}  // namespace
 
 extern "C" {
 
@@ -128,11 +114,12 @@ int fmcw_comm_unique_id(void* id_out) {
   return FMCW_OK;
 }
 
-int fmcw_comm_create(const void* id, int n_ranks, int rank, int device_id, fmcw_comm** out) {
+int fmcw_comm_create(const void* id, int n_ranks, int rank, int device_id, size_t wire_cap, fmcw_comm** out) {
   if (!id || !out) return gfail(FMCW_EINVAL, "null argument");
   *out = nullptr;
   if (n_ranks < 1 || n_ranks > 64 || rank < 0 || rank >= n_ranks)
     return gfail(FMCW_EINVAL, "rank %d of %d (1..64 ranks)", rank, n_ranks);
+  if (wire_cap < 1 || wire_cap > (1u << 26)) return gfail(FMCW_EINVAL, "wire_cap %zu (1..2^26)", wire_cap);
   if (hipSetDevice(device_id) != hipSuccess) {
     (void)hipGetLastError();
     return gfail(FMCW_ENODEV, "device_id %d", device_id);
@@ -143,10 +130,40 @@ int fmcw_comm_create(const void* id, int n_ranks, int rank, int device_id, fmcw_
   c->n_ranks = n_ranks;
   c->rank = rank;
   c->device_id = device_id;
+  c->wire_cap = wire_cap;
   const ncclResult_t r = ncclCommInitRank(&c->comm, n_ranks, uid, rank);
   if (r != ncclSuccess) {
     delete c;
     return gfail(FMCW_EHIP, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  }
+  const size_t msg = (1 + wire_cap) * sizeof(fmcw_det);
+  if (hipMalloc(reinterpret_cast<void**>(&c->wire), msg) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&c->recv), msg * (size_t)n_ranks) != hipSuccess) {
+    (void)hipGetLastError();
+    fmcw_comm_destroy(c);
+    return gfail(FMCW_ENOMEM, "gather buffers (%zu B per rank) failed", msg);
+  }
+  if (n_ranks > 1) {
+    // every rank must size its message alike (send / recv sizes match): one collective check here,
+    // the only host synchronisation of the communicator's life
+    uint64_t* v = nullptr;
+    uint64_t h[2] = {(uint64_t)wire_cap, ~(uint64_t)wire_cap};  // max of both = max and ~min
+    ncclResult_t rr = ncclSuccess;
+    if (hipMalloc(reinterpret_cast<void**>(&v), sizeof h) != hipSuccess ||
+        hipMemcpy(v, h, sizeof h, hipMemcpyHostToDevice) != hipSuccess ||
+        (rr = ncclAllReduce(v, v, 2, ncclUint64, ncclMax, c->comm, nullptr)) != ncclSuccess ||
+        hipMemcpy(h, v, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) {
+      (void)hipGetLastError();
+      if (v) hipFree(v);
+      fmcw_comm_destroy(c);
+      return gfail(FMCW_EHIP, "wire_cap check (all-reduce): %s", ncclGetErrorString(rr));
+    }
+    hipFree(v);
+    if (h[0] != wire_cap || ~h[1] != wire_cap) {
+      fmcw_comm_destroy(c);
+      return gfail(FMCW_EINVAL, "wire_cap differs between ranks (this rank %zu, max %llu, min %llu)", wire_cap,
+                   (unsigned long long)h[0], (unsigned long long)~h[1]);
+    }
   }
   *out = c;
   return FMCW_OK;
@@ -162,20 +179,19 @@ int fmcw_comm_destroy(fmcw_comm* c) {
   return FMCW_OK;
 }
 
-int fmcw_gather_dets(fmcw_comm* c, const fmcw_det* dets_dev, const uint32_t* n_dets_dev, size_t wire_cap,
+int fmcw_gather_dets(fmcw_comm* c, const fmcw_det* dets_dev, size_t det_cap, const uint32_t* n_dets_dev,
                      uint32_t frame_offset, fmcw_det* out_dev, uint32_t* out_n_dev, int root, void* stream) {
-  if (!c || !dets_dev || !n_dets_dev || wire_cap < 1) return gfail(FMCW_EINVAL, "null argument or wire_cap 0");
+  if (!c || !dets_dev || !n_dets_dev) return gfail(FMCW_EINVAL, "null argument");
   if (root < 0 || root >= c->n_ranks) return gfail(FMCW_EINVAL, "root %d of %d ranks", root, c->n_ranks);
   if (c->rank == root && (!out_dev || !out_n_dev)) return gfail(FMCW_EINVAL, "root needs out_dev and out_n_dev");
-  if (wire_cap > (1u << 26)) return gfail(FMCW_EINVAL, "wire_cap %zu too large", wire_cap);
   if (hipSetDevice(c->device_id) != hipSuccess) return gfail(FMCW_EHIP, "hipSetDevice");
-  int rc = ensure_wire(c, wire_cap);
-  if (rc) return rc;
+  const size_t wire_cap = c->wire_cap;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const size_t msg = (1 + wire_cap) * sizeof(fmcw_det);
   const int pack_blocks = (int)std::min<size_t>(1024, (wire_cap + 255) / 256);
-  hipLaunchKernelGGL(k_gather_pack, dim3(pack_blocks), dim3(256), 0, s, dets_dev, n_dets_dev, (uint32_t)wire_cap,
-                     frame_offset, c->wire);
+  hipLaunchKernelGGL(k_gather_pack, dim3(pack_blocks), dim3(256), 0, s, dets_dev,
+                     (uint32_t)std::min<size_t>(det_cap, 0xffffffffu), n_dets_dev, (uint32_t)wire_cap, frame_offset,
+                     c->wire);
   if (hipGetLastError() != hipSuccess) return gfail(FMCW_EHIP, "k_gather_pack launch");
   if (c->rank == root) {
     if (hipMemcpyAsync(reinterpret_cast<char*>(c->recv) + (size_t)root * msg, c->wire, msg, hipMemcpyDeviceToDevice,
@@ -200,6 +216,31 @@ int fmcw_gather_dets(fmcw_comm* c, const fmcw_det* dets_dev, const uint32_t* n_d
                        out_dev, out_n_dev);
     if (hipGetLastError() != hipSuccess) return gfail(FMCW_EHIP, "k_gather_compact launch");
   }
+  return FMCW_OK;
+}
+
+// Single-process test hooks: the pack and compaction kernels without RCCL, so one GPU can check
+// N ranks' messages (counts 0, small, over wire_cap, with losses) against a host model.
+int fmcw_gather_pack_for_test(const fmcw_det* dets_dev, size_t det_cap, const uint32_t* n_dets_dev,
+                              size_t wire_cap, uint32_t frame_offset, fmcw_det* msg_dev, void* stream) {
+  if (!dets_dev || !n_dets_dev || !msg_dev || wire_cap < 1 || wire_cap > (1u << 26))
+    return gfail(FMCW_EINVAL, "null argument or wire_cap out of 1..2^26");
+  const int pack_blocks = (int)std::min<size_t>(1024, (wire_cap + 255) / 256);
+  hipLaunchKernelGGL(k_gather_pack, dim3(pack_blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), dets_dev,
+                     (uint32_t)std::min<size_t>(det_cap, 0xffffffffu), n_dets_dev, (uint32_t)wire_cap, frame_offset,
+                     msg_dev);
+  if (hipGetLastError() != hipSuccess) return gfail(FMCW_EHIP, "k_gather_pack launch");
+  return FMCW_OK;
+}
+
+int fmcw_gather_compact_for_test(const fmcw_det* msgs_dev, int n_ranks, size_t wire_cap, fmcw_det* out_dev,
+                                 uint32_t* out_n_dev, void* stream) {
+  if (!msgs_dev || !out_dev || !out_n_dev || n_ranks < 1 || n_ranks > 64 || wire_cap < 1 || wire_cap > (1u << 26))
+    return gfail(FMCW_EINVAL, "null argument, n_ranks out of 1..64 or wire_cap out of 1..2^26");
+  const int blocks = (int)std::min<size_t>(256, (wire_cap + 255) / 256);
+  hipLaunchKernelGGL(k_gather_compact, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), msgs_dev,
+                     n_ranks, (uint32_t)wire_cap, out_dev, out_n_dev);
+  if (hipGetLastError() != hipSuccess) return gfail(FMCW_EHIP, "k_gather_compact launch");
   return FMCW_OK;
 }
 

@@ -51,18 +51,30 @@ namespace fmcw {
 // raw bits and expands them only when it consumes them: a conversion next to the load would
 // make the prefetch wait for its data at once (fp16 / int16 input, config 5).
 // --------------------------------------------------------------------------------------
+// fetch1 / expand1: one complex sample per lane (k_range_sq's radix-16 first pass).
+template <bool NT>
+__device__ __forceinline__ uint32_t ld_u1(const void* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p));
+  else return *reinterpret_cast<const uint32_t*>(p);
+}
 struct LoadF32 {
   static constexpr int bytes = 8;
   using Raw = float4;
+  using Raw1 = float2;
   __device__ __forceinline__ static Raw fetch(const void* base, size_t idx) {
     return ld_f4<FMCW_NT_CUBE>(reinterpret_cast<const float2*>(base) + idx);
   }
   __device__ __forceinline__ static float4 expand(Raw r) { return r; }
   __device__ __forceinline__ static float4 load2(const void* base, size_t idx) { return fetch(base, idx); }
+  __device__ __forceinline__ static Raw1 fetch1(const void* base, size_t idx) {
+    return ld_f2<FMCW_NT_CUBE>(reinterpret_cast<const float2*>(base) + idx);
+  }
+  __device__ __forceinline__ static float2 expand1(Raw1 r) { return r; }
 };
 struct LoadF16 {
   static constexpr int bytes = 4;
   using Raw = fmcw_u2v;
+  using Raw1 = uint32_t;
   __device__ __forceinline__ static Raw fetch(const void* base, size_t idx) {
     return ld_u2<FMCW_NT_CUBE>(reinterpret_cast<const uint32_t*>(base) + idx);
   }
@@ -72,10 +84,19 @@ struct LoadF16 {
     return make_float4((float)h[0], (float)h[1], (float)h[2], (float)h[3]);
   }
   __device__ __forceinline__ static float4 load2(const void* base, size_t idx) { return expand(fetch(base, idx)); }
+  __device__ __forceinline__ static Raw1 fetch1(const void* base, size_t idx) {
+    return ld_u1<FMCW_NT_CUBE>(reinterpret_cast<const uint32_t*>(base) + idx);
+  }
+  __device__ __forceinline__ static float2 expand1(Raw1 u) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const h2 h = __builtin_bit_cast(h2, u);
+    return make_float2((float)h[0], (float)h[1]);
+  }
 };
 struct LoadI16 {
   static constexpr int bytes = 4;
   using Raw = fmcw_u2v;
+  using Raw1 = uint32_t;
   __device__ __forceinline__ static Raw fetch(const void* base, size_t idx) {
     return ld_u2<FMCW_NT_CUBE>(reinterpret_cast<const uint32_t*>(base) + idx);
   }
@@ -85,6 +106,14 @@ struct LoadI16 {
     return make_float4((float)s[0], (float)s[1], (float)s[2], (float)s[3]);
   }
   __device__ __forceinline__ static float4 load2(const void* base, size_t idx) { return expand(fetch(base, idx)); }
+  __device__ __forceinline__ static Raw1 fetch1(const void* base, size_t idx) {
+    return ld_u1<FMCW_NT_CUBE>(reinterpret_cast<const uint32_t*>(base) + idx);
+  }
+  __device__ __forceinline__ static float2 expand1(Raw1 u) {
+    typedef short s2 __attribute__((ext_vector_type(2)));
+    const s2 s = __builtin_bit_cast(s2, u);
+    return make_float2((float)s[0], (float)s[1]);
+  }
 };
 
 // Corner-turned spectrum element: complex fp32 (8 B) or, with FMCW_SPEC_F16, a half2 (4 B)
@@ -105,6 +134,15 @@ __device__ __forceinline__ float2 ld_spec(const uint32_t* p, float scale) {
   else u = *p;
   const fmcw_h2 h = __builtin_bit_cast(fmcw_h2, u);
   return make_float2((float)h[0] * scale, (float)h[1] * scale);
+}
+
+// Per-call status counters (fmcw.h: status words 2 / 3 of fmcw_enqueue): a thread's count, summed
+// over its wave by shuffles, one atomic per wave that saw any event.  Called once per kernel, by
+// every lane of the wave (after the grid-stride loop).
+__device__ __forceinline__ void status_add(uint32_t* word, uint32_t n) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) n += (uint32_t)__shfl_xor((int)n, d, 64);
+  if (word && n && (threadIdx.x & 63) == 0) atomicAdd(word, n);
 }
 
 // K1 geometry per range-FFT size: T chirps per workgroup, RB = 128/T (1 KiB chunks).
@@ -135,7 +173,7 @@ template <int N, typename LD, bool Q15 = false, bool H16 = false>
 __global__ void __launch_bounds__(RangeGeom<N>::NT)
 __attribute__((amdgpu_waves_per_eu(FMCW_K1_WAVES > 0 && N < 8192 ? FMCW_K1_WAVES : 1)))
 k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* __restrict__ win,
-        const float* __restrict__ chirp_w, int nc, int n_groups, float q15_scale) {
+        const float* __restrict__ chirp_w, int nc, int n_groups, float q15_scale, uint32_t* __restrict__ status) {
   using Gm = RangeGeom<N>;
   constexpr int P = Gm::P, T = Gm::T, RB = Gm::RB, REG = Gm::REG;
   __shared__ __attribute__((aligned(16))) float2 lds[T * REG];
@@ -155,6 +193,7 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
   const int rd0_off = c0 * REG + pad16(r0);
 
   int g = blockIdx.x;
+  uint32_t n_sat = 0;     // Q15: windowed samples this thread saturated
   typename LD::Raw a[8];  // this group's samples, raw (expanded at use)
   // Doppler window of the next chirp, loaded with its samples: a vector load issued after the
   // previous iteration's eight tile stores would make the wait for it (vmcnt counts in issue
@@ -209,12 +248,16 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
         if constexpr (Q15) {
           const int c = (int)(e ? w[m].y : w[m].x);
           const float xi = e ? ax[m].z : ax[m].x, xq = e ? ax[m].w : ax[m].y;
-          auto win16 = [c](float x) {
+          uint32_t clip = 0;  // the sample's saturation_flag (I or Q clipped, window_multiplier.vhd:152-158)
+          auto win16 = [c, &clip](float x) {
             const int y = ((int)x * c + (1 << 14)) >> 14;  // floor: arithmetic shift
-            return (float)min(max(y, -32768), 32767);
+            const int ys = min(max(y, -32768), 32767);
+            clip |= (uint32_t)(ys != y);
+            return (float)ys;
           };
           // 2^-range_shift (the IP's scaling schedule) applies after the integer window
           v[m] = make_float2(win16(xi) * (cw * q15_scale), win16(xq) * (cw * q15_scale));
+          n_sat += clip;
         } else {
           const float we = (e ? w[m].y : w[m].x) * cw;
           v[m] = e ? make_float2(ax[m].z * we, ax[m].w * we) : make_float2(ax[m].x * we, ax[m].y * we);
@@ -264,6 +307,7 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
       else st_f4<FMCW_NT_SPEC_ST>(dst + i * dstep, make_float4(v0.x, v0.y, v1.x, v1.y));
     }
   }
+  if constexpr (Q15) status_add(status, n_sat);  // status word 0: window saturations
 }
 
 // --------------------------------------------------------------------------------------
@@ -280,7 +324,7 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
 template <int N, typename LD>
 __global__ void __launch_bounds__(N / 16) __attribute__((amdgpu_waves_per_eu(1)))
 k_range2(const void* __restrict__ cube, float2* __restrict__ inter, const float* __restrict__ win,
-         const float* __restrict__ chirp_w, int nc, int n_groups, float /* q15_scale: unused */) {
+         const float* __restrict__ chirp_w, int nc, int n_groups, float /* q15_scale */, uint32_t* /* status */) {
   using Gm = RangeGeom<N>;
   constexpr int P = Gm::P, RB = Gm::RB, REG = Gm::REG;
   static_assert(Gm::T == 2 && P >= 128, "two chirps per group, several waves per transform");
@@ -380,6 +424,139 @@ k_range2(const void* __restrict__ cube, float2* __restrict__ inter, const float*
         st_f4<FMCW_NT_SPEC_ST>(inter + off, make_float4(x0[m].x, x0[m].y, x1[m].x, x1[m].y));
       }
     }
+  }
+}
+
+// --------------------------------------------------------------------------------------
+// K1 "sequential pair" k_range_sq<N, LD, V, E> (N >= 2048, round 3).  Same input, window and
+// tiled output (T = 2: the 16-B (chirp 0, chirp 1) element per range bin) as k_range2, but the
+// two chirps of a group go through ONE chirp's worth of LDS one after the other: the first
+// chirp's spectrum waits in registers (V values per thread) while the second is transformed, then
+// both are stored as 16-B pairs straight from registers.  Half the LDS per workgroup doubles the
+// workgroups per CU (N = 8192: two of 68 KiB instead of one of 136 KiB; N = 4096: four), so one
+// workgroup's barriers and LDS passes overlap another's memory phases -- k_range2 at N = 8192 ran
+// one workgroup of 8 waves per CU and was latency-bound (round-2 verdict: 0.53 of HBM).
+//   V = values per thread (16 or 32), P = N / V threads (one transform per workgroup pass);
+//   E = consecutive samples per lane per load: the first pass is a radix-(V/E) Stockham pass on
+//   the E groups j = E t + e, v[m] = x[j + m N/(V/E)] (E = 1: radix 16 from 8-B fp32 / 4-B fp16
+//   loads, so N = 4096 = 16^3 takes two LDS exchanges instead of three; E = 2: 16-B fp32 / 8-B fp16
+//   loads as k_range2).  Then radix-16 LDS passes while more than V points remain per group, and
+//   the last pass into registers: lane t holds X[j + m L] for j = t + P g, whole 1 KiB tiles per
+//   store instruction.
+// The next chirp's raw input is loaded as soon as this chirp's first pass has consumed its
+// registers (one chirp ahead, whatever group it belongs to), so the load overlaps three LDS passes.
+// Replaces the Xilinx range FFT (rtl/src/radar_core.vhd:303-316) + corner turner (:318-327).
+// --------------------------------------------------------------------------------------
+#ifndef FMCW_K1_SQ         // smallest N that runs k_range_sq (0: never)
+#define FMCW_K1_SQ 4096
+#endif
+#ifndef FMCW_K1_SQ_V8192   // values per thread of k_range_sq at N = 8192 (16 or 32)
+#define FMCW_K1_SQ_V8192 16
+#endif
+template <int N, int V> struct SqGeom {
+  static constexpr int P = N / V;
+  static constexpr int T = 2, RB = 64;          // = RangeGeom<N> for N >= 2048
+  static constexpr int REG = padded(N);
+  static constexpr int WAVES = V == 16 ? 4 : 2;  // per SIMD: 16 (V = 16) or 8 (V = 32) waves per CU
+};
+template <int N, typename LD, int V, int E, int W = SqGeom<N, V>::WAVES>
+__global__ void __launch_bounds__(N / V) __attribute__((amdgpu_waves_per_eu(W)))
+k_range_sq(const void* __restrict__ cube, float2* __restrict__ inter, const float* __restrict__ win,
+           const float* __restrict__ chirp_w, int nc, int n_groups, float /* q15_scale */, uint32_t* /* status */) {
+  using Gm = SqGeom<N, V>;
+  constexpr int P = Gm::P, T = Gm::T, RB = Gm::RB;
+  constexpr int M = V / E;                      // first-pass radix
+  constexpr int S0 = N / M;                     // its input stride (= P E)
+  constexpr int LL = vlast_L<N, M, V>();        // sub-transform size before the last pass
+  constexpr int RF = N / LL, GF = V / RF;       // last pass: radix, groups per thread
+  static_assert(RangeGeom<N>::T == T && RangeGeom<N>::RB == RB, "tile format of K2");
+  static_assert(E == 1 || E == 2, "one or two samples per load");
+  static_assert(M <= 16 && (M == 16 || E == 2), "first pass writes whole padded 16-point runs");
+  __shared__ __attribute__((aligned(16))) float2 lds[Gm::REG];
+  const int t0 = threadIdx.x;
+  const int ncb = nc / T;
+
+  // raw input of the next chirp to transform (E = 2: M loads of 2 samples; E = 1: M of 1)
+  using RawT = std::conditional_t<E == 2, typename LD::Raw, typename LD::Raw1>;
+  RawT a[M];
+  float cwn = 1.f;
+  auto fetch = [&](int g, int q) {
+    const int fr = g / ncb;
+    const int cb = g - fr * ncb;
+    const size_t chirp = (size_t)fr * nc + (size_t)cb * T + q;
+    const int t = opaque(t0);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      if constexpr (E == 2) a[m] = LD::fetch(cube, chirp * N + 2 * t + S0 * m);
+      else a[m] = LD::fetch1(cube, chirp * N + t + S0 * m);
+    }
+    if (chirp_w) cwn = chirp_w[__builtin_amdgcn_readfirstlane(cb * T + q)];
+  };
+  // range window of this thread's first-pass samples, held (V floats)
+  float wh[V];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    if constexpr (E == 2) {
+      const float2 w2 = *reinterpret_cast<const float2*>(win + 2 * t0 + S0 * m);
+      wh[2 * m] = w2.x;
+      wh[2 * m + 1] = w2.y;
+    } else {
+      wh[m] = win[t0 + S0 * m];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < V; ++i) asm volatile("" ::"v"(wh[i]));  // complete before the loop (vmcnt order)
+
+  int g = blockIdx.x;
+  if (g < n_groups) fetch(g, 0);
+  for (; g < n_groups; g += gridDim.x) {
+    const int fr = g / ncb;
+    const int cb = g - fr * ncb;
+    float2 X[2][GF][RF];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int t = opaque(t0);
+      const float cw = cwn;
+      __syncthreads();  // the previous transform's last-pass reads are done with lds
+      // first pass from registers: window (x Doppler weight of the chirp), radix M, E groups
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        float2 v[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          float2 x;
+          if constexpr (E == 2) {
+            const float4 x4 = LD::expand(a[m]);
+            x = e ? make_float2(x4.z, x4.w) : make_float2(x4.x, x4.y);
+          } else {
+            x = LD::expand1(a[m]);
+          }
+          const float we = wh[E * m + e] * cw;
+          v[m] = make_float2(x.x * we, x.y * we);
+        }
+        Dft<M>::run(v);
+        float2* d = lds + pad16((E * t + e) * M);
+#pragma unroll
+        for (int m = 0; m < M; ++m) d[m] = v[m];
+      }
+      // the next chirp's input: this group's second chirp, or the next group's first
+      if (q == 0) fetch(g, 1);
+      else if (g + (int)gridDim.x < n_groups) fetch(g + gridDim.x, 0);
+      __syncthreads();
+      vpasses_mid<N, M, P, V>(lds, t);
+      vpass_last<N, LL, P, V>(lds, t, X[q]);
+    }
+    // tile stores: lane t holds range bins d = t + P gg + LL m of both chirps
+    const int t = opaque(t0);
+    const size_t fbase = (size_t)fr * N * nc;
+#pragma unroll
+    for (int gg = 0; gg < GF; ++gg)
+#pragma unroll
+      for (int m = 0; m < RF; ++m) {
+        const int d = t + P * gg + LL * m;
+        const size_t off = fbase + ((size_t)(d / RB) * ncb + cb) * (RB * T) + (size_t)(d % RB) * T;
+        st_f4<FMCW_NT_SPEC_ST>(inter + off, make_float4(X[0][gg][m].x, X[0][gg][m].y, X[1][gg][m].x, X[1][gg][m].y));
+      }
   }
 }
 
@@ -1029,6 +1206,26 @@ k_cfar1d(const float* __restrict__ map, int ns, int n_tiles, int frame0, int til
 __device__ __forceinline__ float sat16(float v) { return fminf(fmaxf(v, -32768.f), 32767.f); }
 __device__ __forceinline__ float2 sat16c(float2 v) { return make_float2(sat16(v.x), sat16(v.y)); }
 __device__ __forceinline__ float2 q16c(float2 v) { return make_float2(sat16(rintf(v.x)), sat16(rintf(v.y))); }
+// the same, counting a sample whose I or Q clipped
+__device__ __forceinline__ float2 q16c_count(float2 v, uint32_t& n) {
+  const float2 r = make_float2(rintf(v.x), rintf(v.y)), q = sat16c(r);
+  n += (uint32_t)(q.x != r.x || q.y != r.y);
+  return q;
+}
+__device__ __forceinline__ float2 sat16c_count(float2 v, uint32_t& n) {
+  const float2 q = sat16c(v);
+  n += (uint32_t)(q.x != v.x || q.y != v.y);
+  return q;
+}
+// RTL-compat Q15 window on an int16 word pair: y = sat16(floor((x c + 2^14) / 2^14)) per
+// component (window_multiplier.vhd:126-158), c = the ROM integer; x c < 2^31 for int16 words.
+__device__ __forceinline__ float2 win_q15c(float2 x, float c, uint32_t& n) {
+  const int ci = (int)c;
+  const int yi = ((int)x.x * ci + (1 << 14)) >> 14, yq = ((int)x.y * ci + (1 << 14)) >> 14;
+  const int si = min(max(yi, -32768), 32767), sq = min(max(yq, -32768), 32767);
+  n += (uint32_t)(si != yi || sq != yq);
+  return make_float2((float)si, (float)sq);
+}
 
 #ifndef FMCW_K2_PREFETCH  // K2 (MTI off): points of the next (tile, rx) unit loaded ahead (0, 8 or 16)
 #define FMCW_K2_PREFETCH 16
@@ -1074,7 +1271,8 @@ template <int NC, int MTI, bool H16 = false, bool FAST = false>
 __global__ void __launch_bounds__(DopplerGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(k2_waves<NC, MTI, FAST>())))
 k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, int ns, int nrx,
           int lgT, int lgRB, int n_tiles, int frame0, int tile0, float* __restrict__ lin_map,
-          float* __restrict__ db_map, int mag_mode, int mti_rtl, Cfar1DArgs cf, DetSink sink) {
+          float* __restrict__ db_map, int mag_mode, int mti_rtl, int q15d, Cfar1DArgs cf, DetSink sink,
+          uint32_t* __restrict__ status) {
   using Gm = DopplerGeom<NC>;
   constexpr int P = Gm::P, WR = Gm::WR, WPB = Gm::WPB, REGD = Gm::REGD, REGM = Gm::REGM;
   constexpr int LR = Gm::LR, LG = Gm::LG;
@@ -1098,11 +1296,17 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
   // Doppler window for this lane's chirps c = t + P m.  MTI off: K1 already applied it
   // (chirp_w), so no registers are spent on it here.  MTI on: the canceller must see the
   // unwindowed spectrum (doppler_notch precedes doppler_fft, radar_core.vhd:329-352).
-  float wv_d[MTI ? 16 : 1];
-  if constexpr (MTI != 0) {
+  // q15d (FMCW_WIN_Q15_RTL, generic kernel only): win_d holds the ROM integers c[n] and the
+  // window is the RTL's integer arithmetic on the spectrum's int16 words, applied here.
+  constexpr bool WIN_K2 = MTI != 0 || !FAST;
+  float wv_d[WIN_K2 ? 16 : 1];
+  if constexpr (WIN_K2) {
+    if (MTI != 0 || q15d) {
 #pragma unroll
-    for (int m = 0; m < 16; ++m) wv_d[m] = win_d[t0 + P * m];
+      for (int m = 0; m < 16; ++m) wv_d[m] = win_d[t0 + P * m];
+    }
   }
+  uint32_t n_wsat = 0, n_msat = 0;  // saturated samples: integer Doppler window; int16 words / MTI
 
   // element (r, c) of the tiled spectrum: ((rb*NCB + c/T)*RB + r%RB)*T + c%T
   auto off_of = [&](uint32_t rbase, uint32_t rin, uint32_t c) -> uint32_t {
@@ -1210,20 +1414,26 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
       for (int m = 0; m < 16; ++m) {
         const int c = t + P * m;
         float2 x = m < NPF ? nxt[m < NPF ? m : 0] : at((uint32_t)c);
+        // RTL-compat words: the corner turner hands the FFT IP's 16-bit output words on
+        // (round half to even, saturate; counted in status word 3)
+        const bool words = !FAST && (mti_rtl || q15d);
+        if (words) x = q16c_count(x, n_msat);
         if constexpr (MTI >= 2) {  // MTI canceller along slow time, zero history (doppler_notch.vhd:72-102)
           float2 x1 = c >= 1 ? at((uint32_t)(c - 1)) : make_float2(0.f, 0.f);
           float2 x2 = make_float2(0.f, 0.f);
           if constexpr (MTI == 3) x2 = c >= 2 ? at((uint32_t)(c - 2)) : make_float2(0.f, 0.f);
-          if (mti_rtl) {  // FMCW_COMPAT_MTI: 16-bit words in, saturating integer difference out
-            x = q16c(x);
+          if (words) {  // 16-bit words in (their own clipping was counted at their own chirp)
             x1 = q16c(x1);
             x2 = q16c(x2);
           }
-          // integers below 2^18 in compat mode: every step below is exact
+          // integers below 2^18 on words: every step below is exact
           x = MTI == 2 ? csub(x, x1) : cadd(csub(x, cscale(x1, 2.f)), x2);
-          if (mti_rtl) x = sat16c(x);
+          if (words) x = sat16c_count(x, n_msat);  // the canceller's saturating output (:76-93)
         }
-        if constexpr (MTI != 0) x = cscale(x, wv_d[m]);
+        if constexpr (WIN_K2) {
+          if (!FAST && q15d) x = win_q15c(x, wv_d[m], n_wsat);  // window_multiplier.vhd:146-158
+          else if (MTI != 0) x = cscale(x, wv_d[m]);
+        }
         v[m] = x;
       }
       Dft<16>::run(v);                       // pass 1: L = 1, no twiddles
@@ -1309,124 +1519,17 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
     }
     pass_sync<false>();  // the region is reused by the next tile
   }
+  if constexpr (!FAST) {
+    if (mti_rtl || q15d) {  // uniform
+      status_add(status, n_wsat);
+      status_add(status ? status + 1 : nullptr, n_msat);
+    }
+  }
 }
 
 // --------------------------------------------------------------------------------------
 // K3: 2-D OS-CFAR (rtl/src/os_cfar_2d.vhd:140-217) -- see cfar2d.hpp.
 // --------------------------------------------------------------------------------------
 #include "cfar2d.hpp"
-
-// --------------------------------------------------------------------------------------
-// K12: K1 + K2 in one persistent launch, spectrum resident in each XCD's L2 -- see fused.hpp.
-// --------------------------------------------------------------------------------------
-#include "fused.hpp"
-
-// --------------------------------------------------------------------------------------
-// K12p: K1 of chunk c beside K2 of chunk c - 1 in one launch (double-buffered) -- see pair.hpp.
-// --------------------------------------------------------------------------------------
-#include "pair.hpp"
-
-
-// --------------------------------------------------------------------------------------
-// Detection ordering: exclusive scan over per-workgroup counts (in workgroup = (frame,
-// range) order), then copy each workgroup's run to its final place.
-// --------------------------------------------------------------------------------------
-// level 1: per 1024-entry block, exclusive scan -> wg_off (block-local) + block sums
-__global__ void __launch_bounds__(1024)
-k_det_scan_blocks(const uint32_t* __restrict__ wg_count, uint32_t* __restrict__ wg_off, int n,
-                  uint32_t* __restrict__ block_sum) {
-  __shared__ int s_wave[1024 / 64 + 2];
-  const int i = blockIdx.x * 1024 + threadIdx.x;
-  const int v = i < n ? (int)wg_count[i] : 0;
-  int total;
-  const int e = block_excl_scan<1024>(v, s_wave, total);
-  if (i < n) wg_off[i] = (uint32_t)e;
-  if (threadIdx.x == 0) block_sum[blockIdx.x] = (uint32_t)total;
-}
-
-// level 2: one workgroup scans the block sums in place (-> block offsets) and the total
-__global__ void __launch_bounds__(1024)
-k_det_scan_top(uint32_t* __restrict__ block_sum, int nb, uint32_t* __restrict__ n_dets,
-               const uint32_t* __restrict__ dropped, const uint32_t* __restrict__ fused_err) {
-  __shared__ int s_wave[1024 / 64 + 2];
-  const int per = (nb + 1023) / 1024;
-  const int b = threadIdx.x * per;
-  const int e = min(b + per, nb);
-  uint32_t s = 0;
-  for (int i = b; i < e; ++i) s += block_sum[i];
-  int total;
-  uint32_t run = (uint32_t)block_excl_scan<1024>((int)s, s_wave, total);
-  for (int i = b; i < e; ++i) {
-    const uint32_t c = block_sum[i];
-    block_sum[i] = run;
-    run += c;
-  }
-  if (threadIdx.x == 0) {
-    n_dets[0] = (uint32_t)total;  // every detection found
-    n_dets[1] = *dropped;         // of which not stored (handle scratch exhausted)
-    // the fused launch gave up (fused.hpp): the list is incomplete, flagged in the top bit
-    if (fused_err && *fused_err) n_dets[1] |= 0x80000000u;
-  }
-}
-
-// One lane per tile; a tile with more than 8 detections (a target's row) is copied by the
-// whole wave, 64 records per step, so one hot tile does not serialise the kernel.
-__global__ void k_det_copy(const fmcw_det* __restrict__ scratch, uint32_t scratch_cap,
-                           const uint32_t* __restrict__ wg_base, const uint32_t* __restrict__ wg_count,
-                           const uint32_t* __restrict__ wg_off, const uint32_t* __restrict__ block_off,
-                           int n, fmcw_det* __restrict__ out, uint32_t cap) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int lane = threadIdx.x & 63;
-  uint32_t c = 0, b = 0, o = 0;
-  if (i < n) {
-    c = wg_count[i];
-    if (c) {
-      b = wg_base[i];
-      o = block_off[i >> 10] + wg_off[i];
-    }
-  }
-  if (c <= 8)
-    for (uint32_t k = 0; k < c; ++k)
-      if (b + k < scratch_cap && o + k < cap) out[o + k] = scratch[b + k];
-  uint64_t big = __ballot(c > 8);
-  while (big) {
-    const int l = __builtin_ctzll(big);
-    big &= big - 1;
-    const uint32_t cl = (uint32_t)__shfl((int)c, l, 64), bl = (uint32_t)__shfl((int)b, l, 64);
-    const uint32_t ol = (uint32_t)__shfl((int)o, l, 64);
-    for (uint32_t k = lane; k < cl; k += 64)
-      if (bl + k < scratch_cap && ol + k < cap) out[ol + k] = scratch[bl + k];
-  }
-}
-
-// --------------------------------------------------------------------------------------
-// Utilities for the stage entry points.
-// --------------------------------------------------------------------------------------
-// inter (tiled) -> spec[fr][r][c] canonical corner-turner order.
-__global__ void k_unblock(const float2* __restrict__ inter, float2* __restrict__ spec, int ns, int nc,
-                          int T, int RB, size_t total) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const size_t per = (size_t)ns * nc;
-  const size_t fr = i / per;
-  const int rem = (int)(i - fr * per);
-  const int r = rem / nc, c = rem - r * nc;
-  const int ncb = nc / T;
-  const size_t off = ((size_t)((r / RB) * ncb + c / T) * RB + (r % RB)) * T + (c % T);
-  spec[i] = inter[fr * per + off];
-}
-
-__global__ void k_magnitude(const float2* __restrict__ iq, float* __restrict__ out, size_t n, int mode) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float2 X = iq[i];
-  if (mode == FMCW_MAG_AMBM) {
-    const float ai = fabsf(X.x), aq = fabsf(X.y);
-    const float mx = fmaxf(ai, aq), mn = fminf(ai, aq);
-    out[i] = mx + floorf(mn * 0.25f) + floorf(mn * 0.125f);
-  } else {
-    out[i] = mag_sqrt(X.x * X.x + X.y * X.y);
-  }
-}
 
 }  // namespace fmcw

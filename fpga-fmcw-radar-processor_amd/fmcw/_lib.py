@@ -26,9 +26,11 @@ MTI_OFF, MTI_2PULSE, MTI_3PULSE = 0, 2, 3
 COMPAT_CFAR, COMPAT_MTI = 1, 2
 SPEC_F32, SPEC_F16 = 0, 1
 COMM_ID_BYTES = 128
-K_RANGE, K_DOPPLER, K_CFAR2D, K_COMPACT, K_FUSED, K_PAIR, K_COUNT = 0, 1, 2, 3, 4, 5, 6
-KERNEL_NAMES = ("k_range", "k_doppler", "k_cfar", "k_compact", "k_fused", "k_pair")
-INFO_FUSED, INFO_FUSED_GROUP, INFO_FUSED_FALLBACKS, INFO_CHUNK, INFO_PAIR_CHUNK = 1, 2, 3, 4, 5
+K_RANGE, K_DOPPLER, K_CFAR2D, K_COMPACT, K_COUNT = 0, 1, 2, 3, 4
+KERNEL_NAMES = ("k_range", "k_doppler", "k_cfar", "k_compact")
+INFO_CHUNK, INFO_RANGE_KERNEL, INFO_WINDOW_SATURATIONS, INFO_WORD_SATURATIONS = 4, 6, 7, 8
+RANGE_KERNELS = ("k_range", "k_range2", "k_range_sq")   # FMCW_INFO_RANGE_KERNEL values 0, 1, 2
+STATUS_WORDS = 4      # FMCW_STATUS_WORDS: n_dets_dev = found, lost, window / word saturations
 
 STATUS_NAMES = {0: "FMCW_OK", -1: "FMCW_EINVAL", -2: "FMCW_ENOMEM", -3: "FMCW_EHIP",
                 -4: "FMCW_EDETCAP", -5: "FMCW_ENODEV"}
@@ -84,7 +86,6 @@ SIGNATURES = {
     "fmcw_cfar": (_I, [_VP, _VP, _SZ, _VP, _SZ, _VP, _VP]),
     "fmcw_set_profiling": (_I, [_VP, _I]),
     "fmcw_get_info": (_I, [_VP, _I, C.POINTER(C.c_int64)]),
-    "fmcw_get_fused_trace": (_I, [_VP, C.POINTER(C.c_uint64), _SZ]),
     "fmcw_kernel_times": (_I, [_VP, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "fmcw_reset_kernel_times": (_I, [_VP]),
     "fmcw_device_alloc": (_I, [_SZ, C.POINTER(_VP), _I]),
@@ -92,9 +93,11 @@ SIGNATURES = {
     "fmcw_memcpy": (_I, [_VP, _VP, _SZ, _I]),
     "fmcw_device_count": (_I, [C.POINTER(_I)]),
     "fmcw_comm_unique_id": (_I, [_VP]),
-    "fmcw_comm_create": (_I, [_VP, _I, _I, _I, C.POINTER(_VP)]),
+    "fmcw_comm_create": (_I, [_VP, _I, _I, _I, _SZ, C.POINTER(_VP)]),
     "fmcw_comm_destroy": (_I, [_VP]),
-    "fmcw_gather_dets": (_I, [_VP, _VP, _VP, _SZ, C.c_uint32, _VP, _VP, _I, _VP]),
+    "fmcw_gather_dets": (_I, [_VP, _VP, _SZ, _VP, C.c_uint32, _VP, _VP, _I, _VP]),
+    "fmcw_gather_pack_for_test": (_I, [_VP, _SZ, _VP, _SZ, C.c_uint32, _VP, _VP]),
+    "fmcw_gather_compact_for_test": (_I, [_VP, _I, _SZ, _VP, _VP, _VP]),
     "fmcw_tws_config_default": (None, [C.POINTER(FmcwTwsConfig)]),
     "fmcw_tws_create": (_I, [C.POINTER(FmcwTwsConfig), C.POINTER(_VP)]),
     "fmcw_tws_destroy": (_I, [_VP]),

@@ -82,15 +82,17 @@ class RcclGather:
     ``unique_id`` (FMCW_COMM_ID_BYTES bytes from ``RcclGather.make_id()`` on one rank) must be
     distributed out of band, e.g. with torch.distributed.broadcast_object_list."""
 
-    def __init__(self, unique_id: bytes, n_ranks: int, rank: int, device: int):
+    def __init__(self, unique_id: bytes, n_ranks: int, rank: int, device: int, wire_cap: int):
+        """wire_cap: record slots per rank message, the same on every rank (fmcw_comm_create
+        checks it with one all-reduce)."""
         lib = L.load()
         if len(unique_id) != L.COMM_ID_BYTES:
             raise ValueError("unique id must be FMCW_COMM_ID_BYTES long")
         buf = C.create_string_buffer(bytes(unique_id), L.COMM_ID_BYTES)
         h = C.c_void_p()
-        L.check(lib.fmcw_comm_create(buf, n_ranks, rank, device, C.byref(h)))
+        L.check(lib.fmcw_comm_create(buf, n_ranks, rank, device, wire_cap, C.byref(h)))
         self._h, self._lib = h, lib
-        self.n_ranks, self.rank = n_ranks, rank
+        self.n_ranks, self.rank, self.wire_cap = n_ranks, rank, wire_cap
 
     @staticmethod
     def make_id() -> bytes:
@@ -98,11 +100,12 @@ class RcclGather:
         L.check(L.load().fmcw_comm_unique_id(buf))
         return buf.raw
 
-    def gather(self, dets_ptr: int, n_dets_ptr: int, wire_cap: int, frame_offset: int,
+    def gather(self, dets_ptr: int, det_cap: int, n_dets_ptr: int, frame_offset: int,
                out_ptr: int | None, out_n_ptr: int | None, root: int = 0, stream: int = 0):
-        """Device pointers; asynchronous on `stream`.  On the root, out holds n_ranks * wire_cap
-        records, out_n [0] records written, [1] records lost (a rank over wire_cap)."""
-        L.check(self._lib.fmcw_gather_dets(self._h, dets_ptr, n_dets_ptr, wire_cap, frame_offset,
+        """Device pointers; asynchronous on `stream`.  det_cap = the capacity of dets (as given to
+        fmcw_enqueue).  On the root, out holds n_ranks * wire_cap records, out_n [0] records
+        written, [1] records lost (beyond det_cap or wire_cap, or lost in a rank's scratch)."""
+        L.check(self._lib.fmcw_gather_dets(self._h, dets_ptr, det_cap, n_dets_ptr, frame_offset,
                                            out_ptr, out_n_ptr, root, stream or None))
 
     def close(self):

@@ -57,6 +57,15 @@ class RadarOutput:
     def det_doppler_bin(self):      # :35
         return self.dets["doppler"]
 
+    # status_overflow (radar_core.vhd:447-456) as counts: samples saturated by the RTL-compat
+    # integer windows, and int16 spectrum words / canceller outputs clipped (fmcw.h status words)
+    window_saturations: int = 0
+    word_saturations: int = 0
+
+    @property
+    def status_overflow(self) -> bool:
+        return bool(self.window_saturations or self.word_saturations)
+
 
 def pack_adc_words(i: np.ndarray, q: np.ndarray) -> np.ndarray:
     """32-bit AXI words {Q[31:16], I[15:0]} (rtl/src/tb_radar_core.vhd:115-118)."""
@@ -148,7 +157,8 @@ class RadarCore:
         compat_rtl: RTL-compat arithmetic (fmcw.h fmcw_compat): any of "cfar" (17-bit integer
         CFAR, os_cfar.vhd:132 / os_cfar_2d.vhd:189-199) and "mti" (int16 saturating canceller,
         doppler_notch.vhd:73-93).  range_shift: range spectrum scaled by 2^-range_shift (the
-        FFT IP's fixed scaling schedule), so that the MTI's 16-bit words are meaningful.
+        FFT IP's fixed scaling schedule), so that the 16-bit spectrum words of the compat MTI and
+        of window="q15_rtl" (integer windows on both axes) are meaningful.
         spectrum: "f32" or "f16", the element type of the internal corner-turned spectrum
         (fmcw.h fmcw_spectrum_dtype: "f16" halves its HBM traffic; map within 2e-3)."""
         lib = L.load()
@@ -215,11 +225,14 @@ class RadarCore:
         if rc == L.FMCW_EDETCAP and det_cap is None:
             return self.process(cube, want_map, det_cap=int(n.value))
         L.check(rc)
-        return RadarOutput(dets=dets[: n.value].copy(), rd_map=rd_map, n_dets=int(n.value))
+        return RadarOutput(dets=dets[: n.value].copy(), rd_map=rd_map, n_dets=int(n.value),
+                           window_saturations=self.info("window_saturations"),
+                           word_saturations=self.info("word_saturations"))
 
     def enqueue(self, cube, n_frames: int, rd_map=None, dets=None, det_cap: int = 0,
                 n_dets=None, stream: int = 0):
-        """Asynchronous, device pointers only (DeviceBuffer / torch CUDA tensors / ints)."""
+        """Asynchronous, device pointers only (DeviceBuffer / torch CUDA tensors / ints).  n_dets:
+        FMCW_STATUS_WORDS (4) uint32 device words: found, lost, window / word saturations."""
         def p(x):
             return x if isinstance(x, int) or x is None else _ptr(x)[0]
         L.check(self._lib.fmcw_enqueue(self._h, p(cube), n_frames, p(rd_map), p(dets), det_cap,
@@ -249,12 +262,13 @@ class RadarCore:
         return {L.KERNEL_NAMES[k]: (ms[k], n[k]) for k in range(L.K_COUNT)}
 
     def info(self, key: str) -> int:
-        """fmcw_get_info: "fused" (1 = the fused range + Doppler kernel runs), "fused_group"
-        (workgroups per XCD), "fused_fallbacks", "chunk", "pair_chunk" (frames per chunk of the
-        paired K1 + K2 launches, 0 when they are off)."""
-        k = {"fused": L.INFO_FUSED, "fused_group": L.INFO_FUSED_GROUP,
-             "fused_fallbacks": L.INFO_FUSED_FALLBACKS, "chunk": L.INFO_CHUNK,
-             "pair_chunk": L.INFO_PAIR_CHUNK}[key]
+        """fmcw_get_info: "chunk" (frames per K1 -> K2 chunk), "range_kernel" (0 k_range,
+        1 k_range2, 2 k_range_sq), "window_saturations" / "word_saturations" (status words 2 / 3
+        of the last process() call: the sticky status_overflow of radar_core.vhd:447-456 as
+        counts)."""
+        k = {"chunk": L.INFO_CHUNK, "range_kernel": L.INFO_RANGE_KERNEL,
+             "window_saturations": L.INFO_WINDOW_SATURATIONS,
+             "word_saturations": L.INFO_WORD_SATURATIONS}[key]
         v = C.c_int64(0)
         L.check(self._lib.fmcw_get_info(self._h, k, C.byref(v)))
         return int(v.value)

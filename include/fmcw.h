@@ -17,13 +17,16 @@
  *   fmcw_det               det_tdata[16:0] / det_range_bin[9:0] / det_doppler_bin[6:0]
  *                          (radar_core.vhd:31-35) + frame index + threshold (dbg_threshold,
  *                          rtl/src/os_cfar_2d.vhd:34, :219)
- *   FMCW_EDETCAP          the sticky status_overflow flag (radar_core.vhd:447-456): the fp32
- *                          datapath cannot saturate, the detection list can overflow
+ *   status words 2, 3     the sticky status_overflow flag (radar_core.vhd:447-456), as counts:
+ *   of fmcw_enqueue        samples saturated by the RTL-compat integer windows (win1 / win2
+ *                          saturation, window_multiplier.vhd:152-158) and int16 spectrum words /
+ *                          canceller outputs clipped (doppler_notch.vhd:75-93).  The fp32 build
+ *                          spec never saturates; FMCW_EDETCAP reports a detection list overflow
  *   fmcw_range_ct          window_multiplier -> xfft_range -> corner_turner (:267-327),
  *                          corner-turned spectrum as the CT emits it (corner_turner.vhd:80)
  *   fmcw_magnitude         magnitude_calc (rtl/src/magnitude_calc.vhd:45-88)
  *   fmcw_cfar              os_cfar_2d / os_cfar on a caller-supplied magnitude map
- *                          (rtl/src/os_cfar_2d.vhd:83-230, rtl/old/os_cfar.vhd:295-380)
+ *                          (rtl/src/os_cfar_2d.vhd:83-230, rtl/old/os_cfar.vhd:98-137)
  *
  * Conventions
  *   - Return value: 0 (FMCW_OK) or a negative fmcw_status.  fmcw_last_error() returns a
@@ -53,10 +56,14 @@
 extern "C" {
 #endif
 
-#define FMCW_ABI_VERSION 4  /* 2: fmcw_config grew compat_rtl, range_shift (27 words, 108 B);
+#define FMCW_ABI_VERSION 5  /* 2: fmcw_config grew compat_rtl, range_shift (27 words, 108 B);
                                3: + spectrum_dtype (28 words, 112 B);
-                               4: FMCW_K_COUNT 5 -> 6 (fmcw_kernel_times fills 6 entries),
-                                  FMCW_INFO_PAIR_CHUNK */
+                               4: FMCW_K_COUNT 5 -> 6, FMCW_INFO_PAIR_CHUNK;
+                               5: n_dets_dev holds FMCW_STATUS_WORDS (4) words (saturation
+                                  counts); the fused / paired kernels are gone (FMCW_K_COUNT 4,
+                                  info keys 1-3 and 5 retired, fmcw_get_fused_trace removed);
+                                  FMCW_WIN_Q15_RTL also windows slow time in integers;
+                                  fmcw_comm_create takes wire_cap, fmcw_gather_dets det_cap */
 
 typedef enum {
   FMCW_OK = 0,
@@ -68,12 +75,15 @@ typedef enum {
 } fmcw_status;
 
 typedef enum { FMCW_IN_F32 = 0, FMCW_IN_F16 = 1, FMCW_IN_I16 = 2 } fmcw_in_dtype;
-/* FMCW_WIN_Q15_RTL (RTL-compat, in_dtype I16 only): the range window in the RTL's integer
+/* FMCW_WIN_Q15_RTL (RTL-compat, in_dtype I16 only): both windows in the RTL's integer
  * arithmetic, y = sat16((x * c[n] + 2^14) >> 14) with the ROM c = round(32767 w) on the
  * mirrored half address (window_multiplier.vhd:43-46, :97-102, :146-158) -- a 2x gain with a
- * +1 LSB bias, so a zero word windows to 1.  The FFTs stay unscaled fp32 and the Doppler window
- * is the fp32 Hamming table (the reference's second window_multiplier sees the IP's block-
- * floating-point output, which the build does not reproduce). */
+ * +1 LSB bias, so a zero word windows to 1.  Fast time: on the ADC words (u_range_window,
+ * radar_core.vhd:267-276).  Slow time (u_doppler_window, :340-349): on the corner-turned
+ * spectrum's 16-bit words -- the range spectrum scaled by 2^-range_shift (the IP's fixed
+ * scaling schedule; pick range_shift so it fits 16 bits), rounded half-to-even and saturated
+ * to int16 -- after the MTI canceller when it is on.  The FFTs stay unscaled fp32.  Saturated
+ * samples are counted in status words 2 (windows) and 3 (spectrum words, canceller). */
 typedef enum { FMCW_WIN_NONE = 0, FMCW_WIN_HAMMING = 1, FMCW_WIN_Q15_RTL = 2 } fmcw_window;
 /* FMCW_MAG_ABS: |X| = sqrt(re^2 + im^2) (with n_rx > 1: sqrt(sum_rx |X_rx|^2), NCI).
  * FMCW_MAG_AMBM: max(|re|,|im|) + floor(min/4) + floor(min/8) (magnitude_calc.vhd:78-81). */
@@ -167,24 +177,20 @@ typedef enum {
   FMCW_K_DOPPLER = 1, /* Doppler window + FFT + magnitude (+NCI) (+1-D CFAR) + map */
   FMCW_K_CFAR2D = 2,  /* 2-D OS-CFAR */
   FMCW_K_COMPACT = 3, /* detection list ordering */
-  FMCW_K_FUSED = 4,   /* K1 + K2 in one launch, spectrum resident in the XCD L2s */
-  FMCW_K_PAIR = 5,    /* K1 of chunk c beside K2 of chunk c - 1 in one launch (double buffer) */
-  FMCW_K_COUNT = 6
+  FMCW_K_COUNT = 4
 } fmcw_kernel_id;
 
-/* fmcw_get_info keys.  FMCW_INFO_FUSED: 1 when fmcw_enqueue runs the fused range + Doppler
- * kernel (one persistent launch; the corner-turned spectrum of each frame stays in one XCD's
- * L2, the reference's on-chip corner turner, corner_turner.vhd:98-166), 0 when it runs K1 ->
- * HBM -> K2.  Chosen at fmcw_create: one rx, MTI off, fp32 Hamming/none window, a frame
- * spectrum <= 2 MiB, a supported (n_range, n_doppler), and a placement check of the launch on
- * this device; environment FMCW_FUSED=0 disables it.  FMCW_INFO_FUSED_GROUP: workgroups per
- * XCD of the fused launch.  FMCW_INFO_FUSED_FALLBACKS: fused launches that gave up (bounded
- * waits expired) and were re-run on K1 + K2 by fmcw_process.  FMCW_INFO_CHUNK: frames per
- * K1 -> K2 chunk.  FMCW_INFO_PAIR_CHUNK: frames per chunk of the paired launches (K1 of chunk c
- * beside K2 of chunk c - 1, double-buffered; opt-in with environment FMCW_PAIR=1 at
- * fmcw_create, one rx, MTI off, |X|, no dB map, no 2-D CFAR, 1024 x 256), 0 when they are off. */
-typedef enum { FMCW_INFO_FUSED = 1, FMCW_INFO_FUSED_GROUP = 2, FMCW_INFO_FUSED_FALLBACKS = 3,
-               FMCW_INFO_CHUNK = 4, FMCW_INFO_PAIR_CHUNK = 5 } fmcw_info_key;
+/* fmcw_get_info keys.  FMCW_INFO_CHUNK: frames per K1 -> K2 chunk.  FMCW_INFO_RANGE_KERNEL: the
+ * range-stage kernel the handle runs: 0 k_range (T chirps per workgroup), 1 k_range2 (two chirps
+ * per thread), 2 k_range_sq (two chirps one after the other through one chirp's LDS; N = 4096,
+ * 8192); environment FMCW_K1=single|dual|seq at fmcw_create caps the choice.
+ * FMCW_INFO_WINDOW_SATURATIONS / FMCW_INFO_WORD_SATURATIONS: status words 2 / 3 of the last
+ * fmcw_process call (fmcw_enqueue callers read them from n_dets_dev). */
+typedef enum { FMCW_INFO_CHUNK = 4, FMCW_INFO_RANGE_KERNEL = 6, FMCW_INFO_WINDOW_SATURATIONS = 7,
+               FMCW_INFO_WORD_SATURATIONS = 8 } fmcw_info_key;
+
+/* Status words of fmcw_enqueue / fmcw_cfar (n_dets_dev). */
+#define FMCW_STATUS_WORDS 4
 
 /* Only the functions below are exported from libfmcw.so (built -fvisibility=hidden). */
 #if defined(__GNUC__)
@@ -204,15 +210,17 @@ int fmcw_destroy(fmcw_handle* h);
 
 /* Full hot path on n_frames frames, device pointers, asynchronous on `stream`
  * (hipStream_t; NULL = default stream).  rd_map may be NULL.  dets may be NULL when
- * cfar_kind == NONE.  n_dets_dev points at TWO device uint32 words:
- *   n_dets_dev[0] = detections found (may exceed det_cap; entries beyond det_cap are
- *                   not written),
- *   n_dets_dev[1] = detections lost because the handle's internal detection scratch
- *                   overflowed (a tile with more than its slot that also found the shared
- *                   overflow region full); bit 31 set = the fused kernel gave up (its
- *                   bounded inter-workgroup waits expired) and the results are incomplete.
- *                   Non-zero means the list is incomplete; fmcw_process returns
- *                   FMCW_EDETCAP in either case (and re-runs a failed fused batch). */
+ * cfar_kind == NONE.  n_dets_dev points at FMCW_STATUS_WORDS device uint32 words, zeroed and
+ * rewritten by every call (it may be NULL only when cfar_kind == NONE; then no status):
+ *   [0] detections found (may exceed det_cap; entries beyond det_cap are not written),
+ *   [1] detections lost because the handle's internal detection scratch overflowed (a tile
+ *       with more than its slot that also found the shared overflow region full).  Non-zero
+ *       means the list is incomplete; fmcw_process returns FMCW_EDETCAP then,
+ *   [2] samples saturated by the RTL-compat integer windows (FMCW_WIN_Q15_RTL, either axis;
+ *       win1 / win2 saturation_flag, window_multiplier.vhd:152-158),
+ *   [3] samples whose int16 spectrum word or canceller output was clipped (FMCW_COMPAT_MTI or
+ *       FMCW_WIN_Q15_RTL; doppler_notch.vhd:75-93).
+ * [2] and [3] stay 0 on the fp32 build spec, which cannot saturate. */
 int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_map,
                  fmcw_det* dets, size_t det_cap, uint32_t* n_dets_dev, void* stream);
 
@@ -232,35 +240,39 @@ int fmcw_cfar(fmcw_handle* h, const float* map, size_t n_frames, fmcw_det* dets,
  * The reference is one FPGA and has no distributed layer; this is the optional gather of
  * frame-sharded detection lists to one root rank.  One process per GPU.  Rank 0 makes the
  * id (fmcw_comm_unique_id), the caller distributes its FMCW_COMM_ID_BYTES bytes out of band,
- * every rank calls fmcw_comm_create (collective).
- * fmcw_gather_dets is stream-ordered and never synchronises with the host: every rank sends
- * a fixed-size message (a 16-B header holding its count, then `wire_cap` record slots) to
- * `root` with ncclSend/ncclRecv, and the root compacts the lists on the device in rank order
- * (= global frame order for contiguous shards).  Each rank's .frame values get `frame_offset`
- * added (its first global frame).  On the root: out_dev holds n_ranks * wire_cap records,
- * out_n_dev[0] = records written, out_n_dev[1] = records not sent because a rank had more
- * than wire_cap (or its n_dets_dev[1] reported scratch losses).  Other ranks may pass NULL
- * out pointers. */
+ * every rank calls fmcw_comm_create (collective) with the SAME wire_cap (record slots per
+ * rank message, 1..2^26; checked with one all-reduce there: FMCW_EINVAL if the ranks differ).
+ * fmcw_gather_dets is stream-ordered, allocates nothing and never synchronises with the host:
+ * every rank sends a fixed-size message (a 16-B header holding its count, then wire_cap record
+ * slots) to `root` with ncclSend/ncclRecv, and the root compacts the lists on the device in
+ * rank order (= global frame order for contiguous shards).  A rank sends min(n_dets_dev[0],
+ * det_cap, wire_cap) records of dets_dev (det_cap = the capacity of dets_dev, as passed to
+ * fmcw_enqueue), each .frame plus `frame_offset` (its first global frame).  On the root:
+ * out_dev holds n_ranks * wire_cap records, out_n_dev[0] = records written, out_n_dev[1] =
+ * records not sent (beyond det_cap or wire_cap, plus the ranks' n_dets_dev[1] scratch
+ * losses).  Other ranks may pass NULL out pointers. */
 #define FMCW_COMM_ID_BYTES 128
 typedef struct fmcw_comm fmcw_comm;
 int fmcw_comm_unique_id(void* id_out);
-int fmcw_comm_create(const void* id, int n_ranks, int rank, int device_id, fmcw_comm** out);
+int fmcw_comm_create(const void* id, int n_ranks, int rank, int device_id, size_t wire_cap,
+                     fmcw_comm** out);
 int fmcw_comm_destroy(fmcw_comm* c);
-int fmcw_gather_dets(fmcw_comm* c, const fmcw_det* dets_dev, const uint32_t* n_dets_dev,
-                     size_t wire_cap, uint32_t frame_offset, fmcw_det* out_dev,
+int fmcw_gather_dets(fmcw_comm* c, const fmcw_det* dets_dev, size_t det_cap,
+                     const uint32_t* n_dets_dev, uint32_t frame_offset, fmcw_det* out_dev,
                      uint32_t* out_n_dev, int root, void* stream);
+/* Single-GPU test hooks of the gather's device side (no RCCL): the rank-local pack into one
+ * message of (1 + wire_cap) records, and the root's compaction of n_ranks such messages laid
+ * end to end in msgs_dev. */
+int fmcw_gather_pack_for_test(const fmcw_det* dets_dev, size_t det_cap, const uint32_t* n_dets_dev,
+                              size_t wire_cap, uint32_t frame_offset, fmcw_det* msg_dev, void* stream);
+int fmcw_gather_compact_for_test(const fmcw_det* msgs_dev, int n_ranks, size_t wire_cap,
+                                 fmcw_det* out_dev, uint32_t* out_n_dev, void* stream);
 
 /* Profiling: when enabled, fmcw_enqueue brackets each kernel launch with hipEvents on
  * its stream; fmcw_kernel_times synchronises and returns, per fmcw_kernel_id, the summed
  * milliseconds and the number of launches since the last reset. */
 int fmcw_set_profiling(fmcw_handle* h, int enable);
 int fmcw_get_info(fmcw_handle* h, int key, int64_t* value);
-/* Diagnostics: with FMCW_FUSED_TRACE=1 in the environment at fmcw_create, the fused kernel
- * records 100 MHz timestamps of its phases, [xcd 0..7][frame k 0..63][event 0..7] (events:
- * range role first WG: frame start, past the wait for the Doppler side, after its ready
- * signal; Doppler role first WG: wait start, ready seen, freed signalled, tile done; range
- * role last WG: after its ready signal).  Copies min(n_words, 4096) words of the last launch. */
-int fmcw_get_fused_trace(fmcw_handle* h, uint64_t* out, size_t n_words);
 int fmcw_kernel_times(fmcw_handle* h, double* ms, uint64_t* launches);
 int fmcw_reset_kernel_times(fmcw_handle* h);
 

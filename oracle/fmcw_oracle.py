@@ -238,9 +238,9 @@ class Cfar2D:
 def cfar_os1d(mag: np.ndarray, p: Cfar1D = Cfar1D()):
     """1-D OS-CFAR along the last (Doppler) axis, circular.
 
-    Refs: p.ref cells each side beyond p.guard guard cells (os_cfar.vhd:330-341),
-    sorted ascending (:349-357), T = alpha * refs[rank] (:364), detect CUT > T
-    (:369).  Build spec differences: circular in Doppler, no
+    Refs: p.ref cells each side beyond p.guard guard cells (rtl/old/os_cfar.vhd:98-109),
+    sorted ascending (:117-125), T = alpha * refs[rank] (:132), detect CUT > T
+    (:137).  Build spec differences: circular in Doppler, no
     17-bit truncation of T, fp32 arithmetic.
 
     Returns (det mask bool, threshold float32) with mag's shape.
@@ -403,6 +403,71 @@ def mti_spectrum_rtl(spec_rc: np.ndarray, mode: int) -> np.ndarray:
     return one(x.real) + 1j * one(x.imag)
 
 
+def spectrum_words(spec_rc: np.ndarray) -> np.ndarray:
+    """The FFT IP's 16-bit output words as the corner turner hands them on: each component of the
+    (scaled) spectrum rounded half-to-even and saturated to int16 (xfft_0.xci: convergent
+    rounding, 16-bit output)."""
+    x = np.asarray(spec_rc)
+    return np.clip(np.rint(x.real), -32768, 32767) + 1j * np.clip(np.rint(x.imag), -32768, 32767)
+
+
+def saturation_counts(cube_i16: np.ndarray, range_shift: int, mti_mode: int = 0, q15_rtl: bool = True,
+                      mti_rtl: bool = False):
+    """RTL-compat status as counts (fmcw.h status words 2, 3 -- the sticky status_overflow of
+    radar_core.vhd:447-456 counted per sample): (window saturations, word saturations) of one
+    frame [rx, chirp, sample, 2].  A sample counts once when its I or Q clips:
+      window: window_multiplier's sat_flag (:152-158) in u_range_window (ADC words) and, with
+              q15_rtl, in u_doppler_window (spectrum words after the canceller);
+      word:   the spectrum rounded to int16 (spectrum_words) and the canceller's saturating
+              output (doppler_notch.vhd:76-93), when the path carries 16-bit words."""
+    x = np.asarray(cube_i16, np.int64)
+    if x.ndim == 3:
+        x = x[None]
+    ns, nc = x.shape[-2], x.shape[-3]
+
+    def win_clips(v, n):            # v [..., n] integers, window along the last axis
+        rom = hamming_q15(n)
+        half = n // 2
+        idx = np.arange(n)
+        c = rom[np.minimum(np.where(idx < half, idx, n - 1 - idx), half - 1)]
+        y = (v * c + (1 << 14)) >> 14
+        return (y < -32768) | (y > 32767)
+
+    wsat = 0
+    words = None
+    if q15_rtl:
+        wsat += int((win_clips(x[..., 0], ns) | win_clips(x[..., 1], ns)).sum())
+        c = window_q15_cube(x)
+        spec = range_ct(c, window=False)
+    else:
+        spec = range_ct(x[..., 0] + 1j * x[..., 1], window=False)
+    spec = spec * 2.0 ** -range_shift
+    nsat = 0
+    if q15_rtl or mti_rtl:
+        r = np.rint(spec.real), np.rint(spec.imag)
+        nsat += int(((np.abs(r[0] + 0.5) > 32767.5) | (np.abs(r[1] + 0.5) > 32767.5)).sum())
+        words = [np.clip(r[0], -32768, 32767).astype(np.int64), np.clip(r[1], -32768, 32767).astype(np.int64)]
+        if mti_mode:
+            out = []
+            clip = np.zeros(words[0].shape, bool)
+            for v in words:
+                v1 = np.zeros_like(v)
+                v1[..., 1:] = v[..., :-1]
+                if mti_mode == 2:
+                    y = v - v1
+                else:
+                    v2 = np.zeros_like(v)
+                    v2[..., 2:] = v[..., :-2]
+                    y = v - 2 * v1 + v2
+                clip |= (y < -32768) | (y > 32767)
+                out.append(np.clip(y, -32768, 32767))
+            nsat += int(clip.sum())
+            words = out
+        if q15_rtl:
+            wsat += int((win_clips(words[0], nc) | win_clips(words[1], nc)).sum())
+    return wsat, nsat
+
+
 DET_DTYPE = np.dtype([("frame", "<u4"), ("range", "<u2"), ("doppler", "<u2"),
                       ("mag", "<f4"), ("threshold", "<f4")])
 
@@ -425,6 +490,24 @@ def detections(det: np.ndarray, mag: np.ndarray, thr: np.ndarray, frame: int = 0
 # ---------------------------------------------------------------------------
 
 
+def doppler_stage(spec: np.ndarray, window: bool = True, mti_mode: int = 0, q15_rtl: bool = False,
+                  mti_rtl: bool = False) -> np.ndarray:
+    """From the (scaled) corner-turned spectrum [..., range, chirp] to the range-Doppler
+    spectrum: MTI canceller (radar_core.vhd:329-338), Doppler window, Doppler FFT (:340-364).
+    mti_rtl / q15_rtl: the canceller on the IP's 16-bit words (mti_spectrum_rtl); q15_rtl also
+    windows those words in the RTL's integer arithmetic (window_q15_rtl along slow time)."""
+    if mti_rtl or q15_rtl:
+        words = spectrum_words(spec)
+        spec = mti_spectrum_rtl(words, mti_mode) if mti_mode else words
+    else:
+        spec = mti(spec, mti_mode)
+    if q15_rtl:
+        nc = spec.shape[-1]
+        spec = window_q15_rtl(spec.real.astype(np.int64), nc) + 1j * window_q15_rtl(spec.imag.astype(np.int64), nc)
+        return doppler_fft(spec, window=False)
+    return doppler_fft(spec, window)
+
+
 def process(cube: np.ndarray, cfar=None, window: bool = True, mti_mode: int = 0,
             q15_rtl: bool = False, range_shift: int = 0, mti_rtl: bool = False):
     """Full hot path for one frame.
@@ -433,8 +516,10 @@ def process(cube: np.ndarray, cfar=None, window: bool = True, mti_mode: int = 0,
     fp64 map 'mag' [range, doppler], the float32 map used by the CFAR, the
     detection mask and the detection list.  With several rx channels the map is
     the non-coherent integration sqrt(sum_rx |X|^2).
-    q15_rtl: cube is int16 [rx, chirp, sample, 2] and the range window is the RTL's integer
-    Q15 arithmetic (window_q15_cube); the Doppler window stays the fp32 table.
+    q15_rtl: cube is int16 [rx, chirp, sample, 2] and both windows are the RTL's integer Q15
+    arithmetic: the range window on the ADC words (window_q15_cube, u_range_window), the
+    Doppler window on the corner-turned spectrum's 16-bit words (spectrum_words, after the MTI
+    canceller; u_doppler_window, radar_core.vhd:340-349).
     """
     if q15_rtl:
         c = window_q15_cube(cube)
@@ -447,11 +532,7 @@ def process(cube: np.ndarray, cfar=None, window: bool = True, mti_mode: int = 0,
             c = c[None]
         spec = range_ct(c, window)
     spec = spec * 2.0 ** -range_shift            # the IP's fixed scaling schedule (exact)
-    if mti_rtl:
-        spec = mti_spectrum_rtl(spec, mti_mode)
-    else:
-        spec = mti(spec, mti_mode)
-    rd = doppler_fft(spec, window)  # [rx, range, doppler]
+    rd = doppler_stage(spec, window, mti_mode, q15_rtl, mti_rtl)  # [rx, range, doppler]
     mag = magnitude(rd, rx_axis=0)
     mag32 = mag.astype(np.float32)
     if cfar is None:

@@ -23,17 +23,20 @@ def test_header_and_binding_agree():
 
 
 def test_header_enums_match_binding():
-    """Kernel ids and info keys: the ctypes constants are the header's (ABI 4 grew FMCW_K_PAIR,
-    so fmcw_kernel_times fills FMCW_K_COUNT = 6 entries, and FMCW_INFO_PAIR_CHUNK)."""
+    """Kernel ids, info keys and the status word count: the ctypes constants are the header's
+    (ABI 5: FMCW_K_COUNT = 4 entries from fmcw_kernel_times, 4 status words in n_dets_dev)."""
     src = L.HEADER_PATH.read_text()
     enum = {k: int(v) for k, v in re.findall(r"\b(FMCW_(?:K|INFO)_[A-Z0-9_]+)\s*=\s*(\d+)", src)}
     assert enum["FMCW_K_COUNT"] == L.K_COUNT == len(L.KERNEL_NAMES)
     for i, name in enumerate(L.KERNEL_NAMES):
         key = {"k_range": "FMCW_K_RANGE", "k_doppler": "FMCW_K_DOPPLER", "k_cfar": "FMCW_K_CFAR2D",
-               "k_compact": "FMCW_K_COMPACT", "k_fused": "FMCW_K_FUSED", "k_pair": "FMCW_K_PAIR"}[name]
+               "k_compact": "FMCW_K_COMPACT"}[name]
         assert enum[key] == i
-    assert enum["FMCW_INFO_CHUNK"] == L.INFO_CHUNK and enum["FMCW_INFO_PAIR_CHUNK"] == L.INFO_PAIR_CHUNK
-    assert re.search(r"#define FMCW_ABI_VERSION 4\b", src)
+    assert enum["FMCW_INFO_CHUNK"] == L.INFO_CHUNK and enum["FMCW_INFO_RANGE_KERNEL"] == L.INFO_RANGE_KERNEL
+    assert enum["FMCW_INFO_WINDOW_SATURATIONS"] == L.INFO_WINDOW_SATURATIONS
+    assert enum["FMCW_INFO_WORD_SATURATIONS"] == L.INFO_WORD_SATURATIONS
+    assert re.search(r"#define FMCW_ABI_VERSION 5\b", src)
+    assert int(re.search(r"#define FMCW_STATUS_WORDS (\d+)", src).group(1)) == L.STATUS_WORDS
 
 
 def test_library_exports_every_symbol(lib_built):
@@ -57,7 +60,7 @@ def test_gfx950_code_object_present(lib_built):
 
 def test_struct_layouts():
     assert C.sizeof(L.FmcwDet) == 16
-    assert C.sizeof(L.FmcwConfig) == 28 * 4          # ABI 3/4 (fmcw.h FMCW_ABI_VERSION)
+    assert C.sizeof(L.FmcwConfig) == 28 * 4          # ABI 3-5 (fmcw.h FMCW_ABI_VERSION)
     assert L.FmcwDet.range.offset == 4 and L.FmcwDet.mag.offset == 8
 
 
@@ -71,7 +74,7 @@ def test_defaults_mirror_radar_core(lib_built):
             cfg.cfar2d_scale_max, cfg.cfar2d_scale_override) == (75, 2, 4, 6, 0)
     assert (cfg.cfar1d_ref, cfg.cfar1d_guard, cfg.cfar1d_rank) == (8, 2, 12)
     assert cfg.cfar1d_alpha == 4.0
-    assert lib_built.fmcw_abi_version() == 4
+    assert lib_built.fmcw_abi_version() == 5
     assert (cfg.compat_rtl, cfg.range_shift, cfg.spectrum_dtype) == (0, 0, L.SPEC_F32)
     assert b"gfx950" in lib_built.fmcw_version()
 
@@ -116,11 +119,15 @@ def test_compat_cfar_needs_integer_alpha(lib_built):
 
 
 def test_gather_argument_checks(lib_built):
-    assert lib_built.fmcw_comm_create(None, 1, 0, 0, None) == L.FMCW_EINVAL
+    assert lib_built.fmcw_comm_create(None, 1, 0, 0, 16, None) == L.FMCW_EINVAL
     idbuf = C.create_string_buffer(L.COMM_ID_BYTES)
     h = C.c_void_p()
-    assert lib_built.fmcw_comm_create(idbuf, 2, 5, 0, C.byref(h)) == L.FMCW_EINVAL
-    assert lib_built.fmcw_gather_dets(None, None, None, 1, 0, None, None, 0, None) == L.FMCW_EINVAL
+    assert lib_built.fmcw_comm_create(idbuf, 2, 5, 0, 16, C.byref(h)) == L.FMCW_EINVAL
+    assert lib_built.fmcw_comm_create(idbuf, 2, 0, 0, 0, C.byref(h)) == L.FMCW_EINVAL      # wire_cap 0
+    assert b"wire_cap" in lib_built.fmcw_last_error()
+    assert lib_built.fmcw_gather_dets(None, None, 1, None, 0, None, None, 0, None) == L.FMCW_EINVAL
+    assert lib_built.fmcw_gather_pack_for_test(None, 1, None, 1, 0, None, None) == L.FMCW_EINVAL
+    assert lib_built.fmcw_gather_compact_for_test(None, 65, 1, None, None, None) == L.FMCW_EINVAL
     assert lib_built.fmcw_comm_destroy(None) == L.FMCW_OK
 
 

@@ -177,25 +177,38 @@ def test_process_parity(gpu, case):
         # MTI (doppler_notch, radar_core.vhd:329-338) enabled: the next row of SURVEY.md 8f
         "mti2_os2d": dict(ns=1024, nc=128, nrx=1, dtype="i16", cfar="os2d", nf=2, recipe="random_target", mti=2),
         "mti3_os1d": dict(ns=512, nc=64, nrx=2, dtype="f32", cfar="os1d", nf=2, recipe="two_targets", mti=3),
-        # RTL-compat integer range window (window_multiplier.vhd:146-158): SURVEY.md 8f row 2
+        # RTL-compat integer windows on both axes (window_multiplier.vhd:146-158; the Doppler one
+        # on the 16-bit spectrum words, range_shift 10 = the IP's scaling so they fit): SURVEY 8f-2
         "q15_rtl_os2d": dict(ns=1024, nc=128, nrx=1, dtype="i16", cfar="os2d", nf=2, recipe="random_target",
-                             window="q15_rtl"),
+                             window="q15_rtl", range_shift=10),
         "q15_rtl_os1d": dict(ns=1024, nc=256, nrx=1, dtype="i16", cfar="os1d", nf=2, recipe="two_targets",
-                             window="q15_rtl"),
+                             window="q15_rtl", range_shift=10),
     }
     k = cfgs[case]
     mti = k.get("mti", 0)
     cube = synth.frames(k["nf"], k["ns"], k["nc"], k["nrx"], k["recipe"], dtype=k["dtype"])
     with RadarCore(N_RANGE=k["ns"], N_DOPPLER=k["nc"], N_RX=k["nrx"], in_dtype=k["dtype"],
                    cfar=k["cfar"], max_frames=k["nf"], mti_bypass=(mti == 0),
-                   NOTCH_MODE=mti or 2, window=k.get("window", "hamming")) as core:
+                   NOTCH_MODE=mti or 2, window=k.get("window", "hamming"),
+                   range_shift=k.get("range_shift", 0)) as core:
         out = core.process(cube)
         # stage exactness: the GPU CFAR on its own map == oracle CFAR on that map
         exact = run_cfar_stage(core, out.rd_map)
+        q15 = k.get("window") == "q15_rtl"
+        # the integer Doppler window works on 16-bit words rounded from the range spectrum: the
+        # reference takes those words from the GPU's own fp32 spectrum (fmcw_range_ct), so a
+        # word's rounding never differs between fp32 and the fp64 oracle
+        spec = run_range_ct(core, cube, k["nf"]) if q15 else None
     cf = O.Cfar1D() if k["cfar"] == "os1d" else O.Cfar2D()
-    q15 = k.get("window") == "q15_rtl"
-    ref_mag = np.stack([O.process(cube[f] if q15 else to_complex(cube[f], k["dtype"]), None, mti_mode=mti,
-                                  q15_rtl=q15)["mag"] for f in range(k["nf"])])
+    if q15:
+        ref_mag = np.stack([O.magnitude(O.doppler_stage(spec[f].astype(np.complex128), mti_mode=mti, q15_rtl=True),
+                                        rx_axis=0) for f in range(k["nf"])])
+        e2e = np.stack([O.process(cube[f], None, mti_mode=mti, q15_rtl=True, range_shift=k["range_shift"])["mag"]
+                        for f in range(k["nf"])])
+        assert rel_err(out.rd_map, e2e) <= 1e-4                    # frame-level vs the fp64 end to end
+    else:
+        ref_mag = np.stack([O.process(to_complex(cube[f], k["dtype"]), None, mti_mode=mti)["mag"]
+                            for f in range(k["nf"])])
     check_map(out.rd_map, ref_mag)
     want = oracle_dets(out.rd_map, cf)
     np.testing.assert_array_equal(out.dets, want)        # fused path, bit-exact

@@ -292,19 +292,28 @@ def test_rccl_gather_one_rank():
     wire = 512
     out = DeviceBuffer(wire * 16)
     on = DeviceBuffer(16)
-    g = RcclGather(RcclGather.make_id(), 1, 0, 0)
+    g = RcclGather(RcclGather.make_id(), 1, 0, 0, wire)
     try:
-        g.gather(dd.ptr, dn.ptr, wire, 1000, out.ptr, on.ptr, 0, 0)
+        g.gather(dd.ptr, n, dn.ptr, 1000, out.ptr, on.ptr, 0, 0)
         got_n = on.download(np.uint32, (2,))
         got = out.download(DET_DTYPE, (n,))
         want = recs.copy()
         want["frame"] += 1000
         assert list(got_n) == [n, 2]
         np.testing.assert_array_equal(got, want)
-        # wire_cap below the count: the first wire_cap records travel, the rest are counted lost
-        g.gather(dd.ptr, dn.ptr, 100, 0, out.ptr, on.ptr, 0, 0)
+        # det_cap below the count (fmcw_enqueue stored only det_cap records): those travel,
+        # the rest are counted lost
+        g.gather(dd.ptr, 100, dn.ptr, 0, out.ptr, on.ptr, 0, 0)
         got_n = on.download(np.uint32, (2,))
         assert list(got_n) == [100, n - 100 + 2]
+        np.testing.assert_array_equal(out.download(DET_DTYPE, (100,)), recs[:100])
+    finally:
+        g.close()
+    # wire_cap below the count: the first wire_cap records travel, the rest are counted lost
+    g = RcclGather(RcclGather.make_id(), 1, 0, 0, 100)
+    try:
+        g.gather(dd.ptr, n, dn.ptr, 0, out.ptr, on.ptr, 0, 0)
+        assert list(on.download(np.uint32, (2,))) == [100, n - 100 + 2]
         np.testing.assert_array_equal(out.download(DET_DTYPE, (100,)), recs[:100])
     finally:
         g.close()
@@ -369,44 +378,11 @@ def test_process_host_staging_is_reused():
     np.testing.assert_array_equal(c.dets, b.dets[b.dets["frame"] < 2])
 
 
-@pytest.mark.parametrize("ns,nc,dtype,cfar,nf,extra", [
-    (1024, 256, "f32", "os1d", 13, {}),                       # BASELINE config 2, 13 frames (uneven over 8 XCDs)
-    (1024, 128, "i16", "os2d", 9, {}),                        # the reference core, 2-D CFAR after the fused map
-    (512, 256, "f16", "os1d", 3, {"magnitude": "ambm"}),
-    (2048, 128, "f32", "none", 2, {"map_kind": "db"}),
-    (1024, 256, "f32", "os1d", 1, {"cfar1d": (6, 1, 9, 3.0)}),
-])
-def test_fused_kernel_matches_k1_k2(monkeypatch, ns, nc, dtype, cfar, nf, extra):
-    """The fused range + Doppler kernel (one launch, spectrum in the XCD L2s) is bit-identical to
-    K1 -> HBM -> K2 (the same arithmetic in the same order), and on parity with the oracle."""
-    cube = synth.frames(nf, ns, nc, 1, "two_targets", dtype=dtype)
-    monkeypatch.setenv("FMCW_FUSED", "1")                     # opt-in path (fmcw.h FMCW_INFO_FUSED)
-    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, in_dtype=dtype, cfar=cfar, max_frames=nf, **extra) as core:
-        assert core.info("fused") == 1 and core.info("fused_group") >= 64
-        fused = core.process(cube)
-        assert core.info("fused_fallbacks") == 0
-    monkeypatch.setenv("FMCW_FUSED", "0")
-    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, in_dtype=dtype, cfar=cfar, max_frames=nf, **extra) as core:
-        assert core.info("fused") == 0
-        split = core.process(cube)
-    np.testing.assert_array_equal(fused.rd_map, split.rd_map)
-    np.testing.assert_array_equal(fused.dets, split.dets)
-    if extra.get("map_kind") != "db" and extra.get("magnitude") != "ambm":
-        ref = np.stack([O.process(to_complex(cube[f], dtype), None)["mag"] for f in range(nf)])
-        check_map(fused.rd_map, ref)
-        if cfar != "none":
-            cf = O.Cfar2D() if cfar == "os2d" else O.Cfar1D(*extra["cfar1d"]) if "cfar1d" in extra else O.Cfar1D()
-            np.testing.assert_array_equal(fused.dets, oracle_dets(fused.rd_map, cf))
-
-
-@pytest.mark.parametrize("env", [{"FMCW_FUSED": "1"}, {"FMCW_PIPE": "1", "FMCW_PIPE_CHUNK": "8"},
-                                 {"FMCW_PIPE": "1", "FMCW_PIPE_CHUNK": "5", "FMCW_PIPE_BUFS": "3"}])
-def test_repeated_launches_and_device_pointers(monkeypatch, env):
-    """Back-to-back launches on device buffers (the bench's pattern), fused kernel or the
-    two-stream K1/K2 chunk pipeline: every launch equals the first, batches of different sizes
-    included, and equals the serial K1 -> K2 path."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+@pytest.mark.parametrize("chunk", [8, 5])
+def test_repeated_launches_and_device_pointers(chunk):
+    """Back-to-back launches on device buffers (the bench's pattern) with small K1 -> K2 chunks
+    (several chunks per call, one short): every launch equals the first, batches of different
+    sizes included, and equals the auto-chunked path."""
     ns, nc, F = 1024, 256, 64
     uniq = synth.frames(8, ns, nc, 1, "random_target", seed=44)
     cube = DeviceBuffer(F * uniq[0].nbytes)
@@ -416,8 +392,8 @@ def test_repeated_launches_and_device_pointers(monkeypatch, env):
     cap = F * 4096
     ddet = DeviceBuffer(cap * 16)
     dn = DeviceBuffer(16)
-    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os1d", max_frames=F) as core:
-        assert core.info("fused") == (1 if "FMCW_FUSED" in env else 0)
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os1d", max_frames=F, chunk_frames=chunk) as core:
+        assert core.info("chunk") == chunk
         runs = []
         for nfr in (F, F, 17, F):
             core.enqueue(cube, nfr, dmap, ddet, cap, dn)
@@ -430,8 +406,6 @@ def test_repeated_launches_and_device_pointers(monkeypatch, env):
         np.testing.assert_array_equal(d, d0[d0["frame"] < nfr])
     for f in range(8, F):
         np.testing.assert_array_equal(m0[f], m0[f % 8])
-    for k in env:
-        monkeypatch.delenv(k)
     with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os1d", max_frames=F) as core:
         core.enqueue(cube, F, dmap, ddet, cap, dn)
         n, _ = (int(v) for v in dn.download(np.uint32, (2,)))

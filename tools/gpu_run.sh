@@ -47,17 +47,6 @@ for s in "$@"; do
     gpu_cfar_tests) run pytest_cfar 600 python -u -m pytest tests -m gpu -v -x -k "cfar or 2d or os2d or config5 or c5 or tb" --timeout 170 --timeout-method thread -p no:cacheprovider ;;
     pmcf_c*) w=${s#pmcf_}; run "pmcf_$w" 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmcf_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
     pmcw_c*) w=${s#pmcw_}; run "pmcw_$w" 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcw_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
-    tests_pair) run pytest_pair 300 python -u -m pytest tests/test_gpu_pair.py -m gpu -v -x --timeout 120 --timeout-method thread -p no:cacheprovider ;;
-    bench_pair) FMCW_PAIR=1 run bench_pair 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
-    pair_sweep)  # paired launches: chunk sizes, and the variant libraries
-      for c in ${PCHUNKS:-24 48 72}; do
-        FMCW_PAIR=1 FMCW_PAIR_CHUNK=$c run "bench_pair_c$c" 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d
-      done
-      for lib in fpga-fmcw-radar-processor_amd/lib/var_*.so; do
-        [ -f "$lib" ] || continue
-        v=$(basename "$lib" .so)
-        FMCW_PAIR=1 FMCW_LIB="$PWD/$lib" run "bench_pair_${v#var_}" 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d
-      done ;;
     bench_libs)  # config-2 bench for every variant library, then the default one again
       for lib in fpga-fmcw-radar-processor_amd/lib/var_*.so; do
         v=$(basename "$lib" .so)
@@ -65,8 +54,6 @@ for s in "$@"; do
       done
       run bench_lib_default 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ${BENCH_ARGS:-} ;;
     bench_f16) run bench_f16 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d --spectrum f16 ;;
-    single_c5) FMCW_K1_SINGLE=1 run single_c5 300 python bench.py --workload c5 --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
-    bench_nopair) FMCW_PAIR=0 run bench_nopair 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
     bench_generic) FMCW_K2_GENERIC=1 run bench_generic 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
     bench_quick) run bench_quick 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
     chunk_sweep)  # config-2 bench per K1/K2 chunk size (frames per launch)
@@ -74,6 +61,23 @@ for s in "$@"; do
         run "bench_chunk$c" 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d --chunk "$c"
       done ;;
     counters) run counters 120 rocprofv3 -L ;;
+    # round 3: one default bench command (config 2 + the config-3 / config-5 sub-records), its
+    # kernel-trace stats and its three PMC passes (tools/pmc_summary.py normalises per frame)
+    prof3) run rocprof3_stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof3" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
+    pmc3_fetch) run pmc3_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc3_fetch" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
+    pmc3_write) run pmc3_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc3_write" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
+    pmc3_sq) run pmc3_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_ACTIVE_INST_ANY -d "$OUT/pmc3_sq" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
+    k1lab)  # K1 variants stand-alone (tools/k1_lab, built on the CPU host): configs 5, 3, 2048
+      run k1lab_c5_3f 120 tools/k1_lab 8192 1024 1 3 1 &&
+      run k1lab_c5_12f 120 tools/k1_lab 8192 1024 1 12 1 &&
+      run k1lab_c3_3f 120 tools/k1_lab 4096 512 4 3 0 &&
+      run k1lab_c3_12f 120 tools/k1_lab 4096 512 4 12 0 ;;
+    chunkc_c*)  # configs 3 / 5: K1 / K2 per-launch times per chunk size (24 frames per step)
+      w=${s#chunkc_}
+      for c in ${CHUNKS:-3 6 12 24}; do
+        run "bench_${w}_chunk$c" 300 python bench.py --workload "$w" --frames 24 --steps 6 --warmup 2 --no-cpu-baseline --no-h2d --chunk "$c"
+      done ;;
+    pmcsq2_c*) w=${s#pmcsq2_}; run "pmcsq2_$w" 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_ACTIVE_INST_ANY -d "$OUT/pmcsq2_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
     prof_c*) w=${s#prof_}; run "rocprof_stats_$w" 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 5 --warmup 2 --no-cpu-baseline --no-h2d ;;
     pmcsq_c*) w=${s#pmcsq_}; run "pmcsq_$w" 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/pmcsq_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
     pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_LDS_BANK_CONFLICT -d "$OUT/pmc_sq" -o run --output-format csv -- python3 tools/ablate.py --frames 256 --steps 2 --variants base ;;

@@ -1,56 +1,98 @@
 #!/usr/bin/env python3
-"""Per-launch HBM traffic from two rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE, each in
-its own run -- MI355X_MICROARCH.md "HBM [CDNA4]": the two do not fit one TCC pass).
+"""Per-frame HBM traffic and SQ instruction counts of the bench's kernels, from rocprofv3 PMC
+passes of ONE bench.py command (MI355X_MICROARCH.md "HBM [CDNA4]": FETCH_SIZE and WRITE_SIZE
+each in its own run; the SQ counters in a third).
 
-Units are KiB.  gfx950 correction: FETCH_SIZE reports half the bytes of a wide coalesced
-streaming read, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.
+Normalisation: every counter is summed over all launches of a kernel in the run and divided by
+the frames that kernel processed in the run (--frames w=N, known from the command: warm-up +
+timed + profiled steps x frames per step), so the numbers do not depend on how the frames were
+split into launches.  bench.py multiplies them by a launch's mean frames.
 
-usage: python tools/pmc_summary.py FETCH_CSV WRITE_CSV --workload c2 --frames-per-launch 32
-       [--out profiles/pmc_r01.json]
+Kernels are assigned to workloads by their template arguments (N / NC differ between configs
+2, 3 and 5): c2 = k_range*<1024>, k_doppler<256>; c3 = k_range*<4096>, k_doppler<512>,
+k_cfar2d<512>; c5 = k_range*<8192>, k_doppler<1024>, k_cfar2d<1024>.
+
+gfx950 correction: FETCH_SIZE reports half the bytes of a wide coalesced streaming read, so it
+is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.  Units of both: KiB.
+
+usage: python tools/pmc_summary.py --fetch F.csv --write W.csv [--sq SQ.csv]
+       --frames c2=5120 --frames c3=112 --frames c5=112 --out profiles/pmc_r03.json
 """
 import argparse
 import collections
 import csv
 import json
+import re
+
+PATTERNS = {
+    "c2": {"k_range": r"k_range\w*<1024,", "k_doppler": r"k_doppler<256,"},
+    "c3": {"k_range": r"k_range\w*<4096,", "k_doppler": r"k_doppler<512,", "k_cfar": r"k_cfar2d<512,"},
+    "c5": {"k_range": r"k_range\w*<8192,", "k_doppler": r"k_doppler<1024,", "k_cfar": r"k_cfar2d<1024,"},
+}
+ALG = {  # algorithmic bytes per frame, fp32 spectrum
+    "c2": {"k_range": 1024 * 256 * 16, "k_doppler": 1024 * 256 * 12},
+    "c3": {"k_range": 4096 * 512 * 4 * 16, "k_doppler": 4096 * 512 * (4 * 8 + 4), "k_cfar": 4096 * 512 * 4},
+    "c5": {"k_range": 8192 * 1024 * 12, "k_doppler": 8192 * 1024 * 12, "k_cfar": 8192 * 1024 * 4},
+}
 
 
-def per_kernel(path, counter):
-    acc = collections.defaultdict(list)
+def read(path):
+    """{kernel name: {counter: [values per dispatch]}}"""
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter:
-            continue
-        name = r["Kernel_Name"]
-        if "fmcw::" not in name:
-            continue
-        short = name.split("fmcw::", 1)[1].split("(", 1)[0]
-        acc[short].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in acc.items()}
+        name = r["Kernel_Name"].replace("fmcw::", "").replace(" ", "")
+        acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return acc
+
+
+def classify(name):
+    for w, pats in PATTERNS.items():
+        for k, p in pats.items():
+            if re.search(p, name):
+                return w, k
+    return None, None
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("fetch_csv")
-    ap.add_argument("write_csv")
-    ap.add_argument("--workload", default="c2")
-    ap.add_argument("--frames-per-launch", type=int, required=True)
-    ap.add_argument("--out", default="profiles/pmc_r01.json")
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--sq", default=None)
+    ap.add_argument("--frames", action="append", default=[], help="workload=frames processed in the run")
+    ap.add_argument("--command", default="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-h2d")
+    ap.add_argument("--out", default="profiles/pmc_r03.json")
     a = ap.parse_args()
-    fetch = per_kernel(a.fetch_csv, "FETCH_SIZE")
-    write = per_kernel(a.write_csv, "WRITE_SIZE")
-    kernels = {}
-    for k in sorted(set(fetch) | set(write)):
-        f = fetch.get(k, 0.0) * 2 * 1024
-        w = write.get(k, 0.0) * 1024
-        kernels[k] = {"fetch_bytes": round(f), "write_bytes": round(w), "hbm_bytes": round(f + w)}
-    rng = next((v for k, v in kernels.items() if k.startswith("k_range")), None)
-    out = {
-        "workload": a.workload,
-        "frames_per_launch": a.frames_per_launch,
-        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of bench.py; "
-                  "KiB -> bytes; FETCH x2 (gfx950 wide-read correction); mean over launches",
-        "k_range_bytes_per_launch": rng["hbm_bytes"] if rng else None,
-        "kernels": kernels,
-    }
+    frames = {k: int(v) for k, v in (x.split("=") for x in a.frames)}
+    tables = [read(a.fetch), read(a.write)] + ([read(a.sq)] if a.sq else [])
+    out = {"method": "rocprofv3 --pmc FETCH_SIZE, --pmc WRITE_SIZE and --pmc SQ_* in separate runs of `"
+                     + a.command + "`; per kernel: sum over its launches / frames it processed; "
+                     "FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes",
+           "frames": frames, "workloads": {}}
+    for t in tables:
+        for name, ctrs in t.items():
+            w, k = classify(name)
+            if not w or w not in frames:
+                continue
+            ent = out["workloads"].setdefault(w, {"kernels": {}})["kernels"].setdefault(k, {"name": name})
+            for c, vals in ctrs.items():
+                tot = sum(vals)
+                if c == "FETCH_SIZE":
+                    ent["fetch_bytes_per_frame"] = tot * 2 * 1024 / frames[w]
+                elif c == "WRITE_SIZE":
+                    ent["write_bytes_per_frame"] = tot * 1024 / frames[w]
+                else:
+                    ent[c + "_per_frame"] = tot / frames[w]
+                ent["launches"] = len(vals)
+    for w, d in out["workloads"].items():
+        for k, e in d["kernels"].items():
+            if "fetch_bytes_per_frame" in e and "write_bytes_per_frame" in e:
+                e["hbm_bytes_per_frame"] = e["fetch_bytes_per_frame"] + e["write_bytes_per_frame"]
+                e["algorithmic_bytes_per_frame"] = ALG[w].get(k)
+                if e["algorithmic_bytes_per_frame"]:
+                    e["traffic_over_algorithmic"] = round(e["hbm_bytes_per_frame"] / e["algorithmic_bytes_per_frame"], 4)
+            for key in list(e):
+                if isinstance(e[key], float):
+                    e[key] = round(e[key], 1)
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
