@@ -147,8 +147,6 @@ int fail(int code, const char* fmt, ...) {
 
 bool pow2(uint32_t x) { return x && !(x & (x - 1)); }
 
-constexpr int kWavesPerBlock = 4;  // DopplerGeom<NC>::WPB: wave tiles per K2 / 1-D CFAR workgroup
-static_assert(kWavesPerBlock == DopplerGeom<256>::WPB, "host and kernel tile geometry");
 
 struct PendingEvent {
   int kid;
@@ -441,7 +439,8 @@ int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipS
   // 1-D on a caller map (fmcw_cfar); inside fmcw_enqueue the 1-D CFAR is fused into K2
   const DopplerInfo di = doppler_info(c.n_doppler);
   const int n_tiles = nf * (int)(c.n_range / di.WR);
-  const int grid = std::min((n_tiles + kWavesPerBlock - 1) / kWavesPerBlock, h->grid_doppler);
+  const int wpb = di.NT / 64;  // DopplerGeom<NC>::WPB: wave tiles per workgroup
+  const int grid = std::min((n_tiles + wpb - 1) / wpb, h->grid_doppler);
   ProfScope ps(h, FMCW_K_CFAR2D, s);
   hipLaunchKernelGGL(cfar1_fn(c.n_doppler), dim3(grid), dim3(di.NT), 0, s, map_chunk, (int)c.n_range,
                      n_tiles, frame0, tile0, cfar1_args(c), sink);
@@ -556,7 +555,7 @@ uint32_t auto_chunk(const fmcw_handle* h, size_t frame_inter) {
   const fmcw_config& c = h->cfg;
   constexpr size_t kMallBudget = 192u << 20;
   size_t ch = std::max<size_t>(1, kMallBudget / frame_inter);
-  const size_t waves = (size_t)h->grid_doppler * kWavesPerBlock;
+  const size_t waves = (size_t)h->grid_doppler * (doppler_info(c.n_doppler).NT / 64);
   const size_t tpf = (size_t)c.n_range / doppler_info(c.n_doppler).WR;
   if (waves % tpf == 0) {
     const size_t unit = waves / tpf;  // frames per full K2 round
@@ -732,7 +731,8 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
     if (c.cfar_kind == FMCW_CFAR_OS2D && !lin) lin = h->lin_scratch;
     {
       const int n_tiles = nf * (int)(c.n_range / di.WR);
-      const int grid = std::min((n_tiles + kWavesPerBlock - 1) / kWavesPerBlock, h->grid_doppler);
+      const int wpb = di.NT / 64;  // DopplerGeom<NC>::WPB
+      const int grid = std::min((n_tiles + wpb - 1) / wpb, h->grid_doppler);
       ProfScope ps(h, FMCW_K_DOPPLER, s);
       hipLaunchKernelGGL(di.fn, dim3(grid), dim3(di.NT), 0, s, h->inter, h->win_d, (int)c.n_range,
                          (int)c.n_rx, h->lgT, h->lgRB, n_tiles, (int)f0, (int)(f0 * (c.n_range / di.WR)), lin,

@@ -35,7 +35,7 @@ RangeFn range2_fn(int dtype) {
 // (values per thread V, samples per load E, waves per SIMD W), tools/k1_lab.hip
 template <int N> struct SqPick;
 template <> struct SqPick<4096> { static constexpr int V = 16, E = 1, W = 3; };
-template <> struct SqPick<8192> { static constexpr int V = 16, E = 2, W = 4; };
+template <> struct SqPick<8192> { static constexpr int V = 16, E = 2, W = 3; };
 template <int N>
 RangeInfo range_sq(int dtype) {
   using S = SqPick<N>;

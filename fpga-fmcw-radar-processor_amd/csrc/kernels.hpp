@@ -747,10 +747,15 @@ __device__ __forceinline__ void load_cells(const float* base, int o0, float (&v)
 // --------------------------------------------------------------------------------------
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
+#ifndef FMCW_K2_WPB_1024  // K2 / 1-D CFAR waves per workgroup at NC = 1024 (4 or 8)
+#define FMCW_K2_WPB_1024 4
+#endif
 template <int NC> struct DopplerGeom {
   static constexpr int P = NC / 16;                     // lanes per range row (16 cells each)
   static constexpr int WR = 64 / P;                     // range rows per wave tile
-  static constexpr int WPB = 4;                         // waves per workgroup (independent)
+  // waves per workgroup (independent; a workgroup's waves take consecutive row groups of one
+  // frame, so together they read WPB x WR x T x 8 B of every 1 KiB spectrum tile)
+  static constexpr int WPB = NC >= 1024 ? FMCW_K2_WPB_1024 : 4;
   static constexpr int NT = 64 * WPB;
   static constexpr int REGD = padded(NC) + 4;           // complex per range row (FFT)
   static constexpr int REGM = mrow_floats<NC>();        // floats per magnitude row

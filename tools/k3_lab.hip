@@ -1,0 +1,192 @@
+// k3_lab.hip -- stand-alone timing / exactness harness for the 2-D OS-CFAR (K3) variants at
+// BASELINE config 5's map geometry (8192 range x 1024 Doppler, 2-D CFAR with the reference
+// window of rtl/src/os_cfar_2d.vhd as instantiated at radar_core.vhd:376-382).
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -o tools/k3_lab tools/k3_lab.hip
+// Run:   tools/k3_lab [frames=16] [reps=5] [ns=8192]
+// Synthetic map: Rayleigh noise (|complex Gaussian|) plus point targets with Hamming-like
+// sidelobes; every variant's detection list (per tile: count + records) must equal the
+// production kernel's, and each variant's average launch time is reported.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../fpga-fmcw-radar-processor_amd/csrc/kernels.hpp"
+
+using namespace fmcw;
+
+#define CK(x)                                                                              \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) {                                                                \
+      std::fprintf(stderr, "%s: %s (line %d)\n", #x, hipGetErrorString(e_), __LINE__);     \
+      std::exit(3);                                                                        \
+    }                                                                                      \
+  } while (0)
+
+constexpr int NC = 1024;
+using Cfar2Fn = void (*)(const float*, int, int, int, int, int, Cfar2DArgs, DetSink);
+
+__device__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+// Rayleigh magnitude (sigma 1000) + targets: every 512th range row has a target at Doppler
+// (row * 37) % NC of amplitude 1e6 with a 3 x 5 neighbourhood at 1e4
+__global__ void k_fill_map(float* m, int ns, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t h1 = hash32((uint32_t)i * 2u + 1u), h2 = hash32((uint32_t)i * 2u + 2u);
+    const float u1 = ((float)(h1 >> 8) + 0.5f) / 16777216.f, u2 = (float)(h2 >> 8) / 16777216.f;
+    float v = 1000.f * sqrtf(-2.f * logf(u1));  // Rayleigh: |N(0,1) + i N(0,1)|
+    (void)u2;
+    const int d = (int)(i % NC);
+    const size_t rr = i / NC;
+    const int r = (int)(rr % ns);
+    const int rt = (r + 2) / 512 * 512;  // nearest target row
+    const int dt = (rt * 37) % NC;
+    const int dr = r - rt, dd = ((d - dt + NC + NC / 2) % NC) - NC / 2;
+    if (rt > 0 && rt < ns && abs(dr) <= 1 && abs(dd) <= 2) v = (dr == 0 && dd == 0) ? 1e6f : 1e4f;
+    m[i] = v;
+  }
+}
+
+struct Var {
+  std::string name;
+  Cfar2Fn fn;
+};
+
+int steps_model(int nf, int tpf, int grid, int tr, int hr) {  // = fmcw_api.hip cfar2_steps_model
+  int best = 1;
+  double best_cost = 1e300;
+  for (int S = 1; S <= std::min(64, tpf); ++S) {
+    const long strips = (long)nf * ((tpf + S - 1) / S);
+    const long rounds = (strips + grid - 1) / std::max(1, grid);
+    const double cost = (double)rounds * (1.5 * S + (double)hr / tr);
+    if (cost < best_cost - 1e-9) {
+      best_cost = cost;
+      best = S;
+    }
+  }
+  return best;
+}
+
+int main(int argc, char** argv) {
+  const int nf = argc > 1 ? std::atoi(argv[1]) : 16;
+  const int reps = argc > 2 ? std::atoi(argv[2]) : 5;
+  const int ns = argc > 3 ? std::atoi(argv[3]) : 8192;
+  std::vector<Var> vars = {{"k_cfar2d one-stage screen", k_cfar2d<NC, 6, 2, 0>},
+                           {"k_cfar2d two-stage screen", k_cfar2d<NC, 6, 2, 1>}};
+#ifdef K3_LAB_VARIANTS
+  K3_LAB_VARIANTS
+#endif
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, 0));
+  const int n_cu = prop.multiProcessorCount;
+  // the reference core's 2-D CFAR parameters (fmcw_api.hip cfar2_args with the defaults)
+  Cfar2DArgs a{};
+  a.gr = 1;
+  a.gd = 2;
+  a.hr = 5;
+  a.hd = 6;
+  a.n_ref = 11 * 13 - 3 * 5;
+  a.rank = a.n_ref * 75 / 100;
+  a.sc_min = 2.f;
+  a.sc_nom = 4.f;
+  a.sc_max = 6.f;
+  a.override_ = 0;
+  a.compat = 0;
+  a.s_min = 2.f;
+  const size_t smem = cfar2d_smem_bytes<NC>(a.hr);
+  const size_t cells = (size_t)nf * ns * NC;
+  float* map;
+  CK(hipMalloc(&map, cells * 4));
+  hipLaunchKernelGGL(k_fill_map, dim3(8192), dim3(256), 0, 0, map, ns, cells);
+  const int WR = DopplerGeom<NC>::WR;
+  const int tiles = nf * ns / WR;
+  const uint32_t slot_cap = 32;
+  const uint32_t ovf = (uint32_t)std::max<size_t>(cells / 64, 65536);
+  const uint32_t cap = (uint32_t)tiles * slot_cap + ovf;
+  DetSink sink{};
+  CK(hipMalloc(&sink.scratch, (size_t)cap * sizeof(fmcw_det)));
+  CK(hipMalloc(&sink.counter, 16));
+  CK(hipMalloc(&sink.wg_base, tiles * 4));
+  CK(hipMalloc(&sink.wg_count, tiles * 4));
+  sink.cap = cap;
+  sink.slot_cap = slot_cap;
+  sink.ovf_base = (uint32_t)tiles * slot_cap;
+  std::vector<uint32_t> ref_cnt, ref_base;
+  std::vector<fmcw_det> ref_sc;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::printf("map %d frames x %d x %d, K3 smem %zu B\n", nf, ns, NC, smem);
+  for (size_t vi = 0; vi < vars.size(); ++vi) {
+    const Var& v = vars[vi];
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(v.fn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+    int per_cu = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(v.fn), 256, smem));
+    const int grid_max = std::max(1, per_cu) * n_cu;
+    const int tpf = (ns / WR + 3) / 4;
+    const int steps = steps_model(nf, tpf, grid_max, WR * 4, a.hr);
+    const int n_strips = nf * ((tpf + steps - 1) / steps);
+    const int grid = std::min(n_strips, grid_max);
+    CK(hipMemset(sink.counter, 0, 16));
+    CK(hipMemset(sink.wg_count, 0, tiles * 4));
+    hipLaunchKernelGGL(v.fn, dim3(grid), dim3(256), smem, 0, map, ns, n_strips, steps, 0, 0, a, sink);
+    CK(hipGetLastError());
+    CK(hipDeviceSynchronize());
+    std::vector<uint32_t> cnt(tiles), base(tiles), ctr(4);
+    std::vector<fmcw_det> sc(cap);
+    CK(hipMemcpy(cnt.data(), sink.wg_count, tiles * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(base.data(), sink.wg_base, tiles * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(sc.data(), sink.scratch, (size_t)cap * sizeof(fmcw_det), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(ctr.data(), sink.counter, 16, hipMemcpyDeviceToHost));
+    size_t ndet = 0;
+    for (int t = 0; t < tiles; ++t) ndet += cnt[t];
+    bool same = true;
+    if (vi == 0) {
+      ref_cnt = cnt;
+      ref_base = base;
+      ref_sc = sc;
+    } else {
+      for (int t = 0; t < tiles && same; ++t) {
+        if (cnt[t] != ref_cnt[t]) {
+          std::printf("  tile %d: %u detections vs %u\n", t, cnt[t], ref_cnt[t]);
+          same = false;
+          break;
+        }
+        for (uint32_t k = 0; k < cnt[t]; ++k)
+          if (std::memcmp(&sc[base[t] + k], &ref_sc[ref_base[t] + k], sizeof(fmcw_det)) != 0) {
+            std::printf("  tile %d record %u differs\n", t, k);
+            same = false;
+            break;
+          }
+      }
+    }
+    float tot = 0;
+    for (int r = 0; r < reps; ++r) {
+      CK(hipMemset(sink.counter, 0, 16));
+      CK(hipEventRecord(e0, 0));
+      hipLaunchKernelGGL(v.fn, dim3(grid), dim3(256), smem, 0, map, ns, n_strips, steps, 0, 0, a, sink);
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      tot += ms;
+    }
+    std::printf("%-34s grid %5d (%d/CU) steps %2d  %8.1f us per launch (%.1f us/frame)  dets %zu dropped %u  %s\n",
+                v.name.c_str(), grid, per_cu, steps, tot / reps * 1e3, tot / reps * 1e3 / nf, ndet, ctr[1],
+                vi == 0 ? "(reference)" : same ? "IDENTICAL" : "DIFFERENT");
+    std::fflush(stdout);
+  }
+  return 0;
+}
