@@ -214,167 +214,6 @@ __device__ __forceinline__ uint32_t cfar2d_screen16(const RowRing& rr, int rl, i
   return bits;
 }
 
-// The same screen with its window rows split over L adjacent, aligned lanes (lane `sub` takes
-// rows dr = -hr + sub, every L-th), the packed counts summed over the L lanes by shuffles: the
-// stage-2 form below, where a few blocks get the whole workgroup.  L = 1 is cfar2d_screen16.
-template <int NC, int HD, int GD>
-__device__ __forceinline__ uint32_t cfar2d_screen16_split(const RowRing& rr, int rl, int d0, const Cfar2DArgs& a,
-                                                          int need, int sub, int L) {
-  constexpr int W = 16 + 2 * HD;
-  constexpr int O0 = floor4(-HD);
-  constexpr int NV = (W + (-HD - O0) + 3) / 4;
-  constexpr int SEG = HD - GD, NPS = SEG / 2;
-  const float* lb = rr.row(rl + a.hr) + midx(d0);
-  const float inv_s = 1.0f / a.s_min;
-  u16x2 ck[8], nlt[8];
-  {
-    float c[16];
-    load_cells<4>(lb, 0, c);
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      const uint32_t k0 = min((__float_as_uint(c[2 * p] * inv_s) + 8u) >> 16, 0x7fffu) + 1u;
-      const uint32_t k1 = min((__float_as_uint(c[2 * p + 1] * inv_s) + 8u) >> 16, 0x7fffu) + 1u;
-      ck[p] = __builtin_bit_cast(u16x2, k0 | (k1 << 16));
-      nlt[p] = (u16x2)(0);
-    }
-  }
-  for (int dr = -a.hr + sub; dr <= a.hr; dr += L) {
-    float v[4 * NV];
-    load_cells<NV>(rr.row(rl + a.hr + dr) + midx(d0), O0, v);
-    u16x2 P[W - 2];
-    {
-      uint32_t V[W - 1];
-#pragma unroll
-      for (int k = 0; k < W - 1; ++k)
-        V[k] = __builtin_amdgcn_perm(__float_as_uint(v[-HD - O0 + k + 1]), __float_as_uint(v[-HD - O0 + k]),
-                                     0x07060302u);
-#pragma unroll
-      for (int k = 0; k < W - 2; ++k)
-        P[k] = __builtin_elementwise_max(__builtin_bit_cast(u16x2, V[k]), __builtin_bit_cast(u16x2, V[k + 1]));
-    }
-    if (dr >= -a.gr && dr <= a.gr) {
-#pragma unroll
-      for (int p = 0; p < 8; ++p)
-#pragma unroll
-        for (int j = 0; j < NPS; ++j) {
-          nlt[p] += (u16x2)(P[2 * p + 2 * j] - ck[p]) >> (unsigned short)15;
-          nlt[p] += (u16x2)(P[2 * p + HD + GD + 1 + 2 * j] - ck[p]) >> (unsigned short)15;
-        }
-    } else {
-#pragma unroll
-      for (int p = 0; p < 8; ++p)
-#pragma unroll
-        for (int j = 0; j < HD; ++j) nlt[p] += (u16x2)(P[2 * p + 2 * j] - ck[p]) >> (unsigned short)15;
-    }
-  }
-  for (int x = 1; x < L; x <<= 1)  // the block's L lanes are adjacent and aligned
-#pragma unroll
-    for (int p = 0; p < 8; ++p)
-      nlt[p] += __builtin_bit_cast(u16x2, __shfl_xor(__builtin_bit_cast(int, nlt[p]), x, 64));
-  const int n_guard = 2 * a.gr + 1;
-  const int np = (2 * a.hr + 1 - n_guard) * HD + n_guard * 2 * NPS;
-  uint32_t bits = 0;
-#pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    bits |= (np - (int)nlt[p].x < need ? 1u : 0u) << (2 * p);
-    bits |= (np - (int)nlt[p].y < need ? 1u : 0u) << (2 * p + 1);
-  }
-  return bits;
-}
-
-// Stage 1 of the two-stage phase A: the pair screen with ONE key per half lane (the largest of
-// its 8 CUTs' keys) instead of one per CUT.  A larger key only lowers each count, so a CUT this
-// bound rejects, cfar2d_screen16 rejects too; but with the key shared, a pair's comparison
-// serves every CUT of the half: per window row 9 packed compares per half (the even pair starts
-// the CUTs use) and a sliding sum of 6, instead of 48 packed compare-and-adds.  On noise the
-// largest of 8 cuts / s_min still sits below most pair maxima, so most lanes reject all 16 cells
-// here; the others go through cfar2d_screen16_split (stage 2).  Returns the CUTs NOT rejected.
-template <int NC, int HD, int GD>
-__device__ __forceinline__ uint32_t cfar2d_screen_shared(const RowRing& rr, int rl, int d0, const Cfar2DArgs& a,
-                                                         int need) {
-  static_assert(HD <= MH, "the window stays inside the row halos");
-  constexpr int W = 16 + 2 * HD;
-  constexpr int O0 = floor4(-HD);
-  constexpr int NV = (W + (-HD - O0) + 3) / 4;
-  constexpr int SEG = HD - GD, NPS = SEG / 2;
-  constexpr int R = HD + GD + 1;              // guard row: offset of the right segment's pairs
-  const float* lb = rr.row(rl + a.hr) + midx(d0);
-  const float inv_s = 1.0f / a.s_min;
-  u16x2 K2[2];                                // the half's shared (key + 1), in both halves
-  {
-    float c[16];
-    load_cells<4>(lb, 0, c);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      uint32_t m = 0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) m = max(m, __float_as_uint(c[8 * h + i]));
-      // key(max cut / s_min) = max of the keys (monotone)
-      const uint32_t k = min((__float_as_uint(__uint_as_float(m) * inv_s) + 8u) >> 16, 0x7fffu) + 1u;
-      K2[h] = __builtin_bit_cast(u16x2, k | (k << 16));
-    }
-  }
-  u16x2 nlt[8];
-#pragma unroll
-  for (int p = 0; p < 8; ++p) nlt[p] = (u16x2)(0);
-  for (int dr = -a.hr; dr <= a.hr; ++dr) {
-    float v[4 * NV];
-    load_cells<NV>(rr.row(rl + a.hr + dr) + midx(d0), O0, v);
-    u16x2 P[W - 2];
-    {
-      uint32_t V[W - 1];
-#pragma unroll
-      for (int k = 0; k < W - 1; ++k)
-        V[k] = __builtin_amdgcn_perm(__float_as_uint(v[-HD - O0 + k + 1]), __float_as_uint(v[-HD - O0 + k]),
-                                     0x07060302u);
-#pragma unroll
-      for (int k = 0; k < W - 2; ++k)
-        P[k] = __builtin_elementwise_max(__builtin_bit_cast(u16x2, V[k]), __builtin_bit_cast(u16x2, V[k + 1]));
-    }
-    // B[h][k] = (not-counted bit of pair start k, of k + 1) under half h's key; CUT pair p
-    // (half h = p / 4) sums B[h][2p + 2j] over its window's pair starts
-    if (dr >= -a.gr && dr <= a.gr) {  // guard row (uniform branch): segments at 2p + 2j, 2p + R + 2j
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        u16x2 B[W - 2];
-#pragma unroll
-        for (int k = 8 * h; k < W - 2 && k <= 8 * h + 6 + R + 2 * (NPS - 1); ++k)
-          B[k] = (u16x2)(P[k] - K2[h]) >> (unsigned short)15;
-#pragma unroll
-        for (int p = 4 * h; p < 4 * h + 4; ++p)
-#pragma unroll
-          for (int j = 0; j < NPS; ++j) nlt[p] += B[2 * p + 2 * j] + B[2 * p + R + 2 * j];
-      }
-    } else {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        u16x2 B[W - 2];
-#pragma unroll
-        for (int k = 8 * h; k <= 8 * h + 6 + 2 * (HD - 1); k += 2) B[k] = (u16x2)(P[k] - K2[h]) >> (unsigned short)15;
-        // sliding window of HD even pair starts: the first CUT pair's sum, then +new -old
-        u16x2 s = B[8 * h];
-#pragma unroll
-        for (int j = 1; j < HD; ++j) s += B[8 * h + 2 * j];
-        nlt[4 * h] += s;
-#pragma unroll
-        for (int p = 4 * h + 1; p < 4 * h + 4; ++p) {
-          s += B[2 * p + 2 * (HD - 1)] - B[2 * p - 2];
-          nlt[p] += s;
-        }
-      }
-    }
-  }
-  const int n_guard = 2 * a.gr + 1;
-  const int np = (2 * a.hr + 1 - n_guard) * HD + n_guard * 2 * NPS;
-  uint32_t bits = 0;
-#pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    bits |= (np - (int)nlt[p].x < need ? 1u : 0u) << (2 * p);
-    bits |= (np - (int)nlt[p].y < need ? 1u : 0u) << (2 * p + 1);
-  }
-  return bits;
-}
-
 // Candidate test of one screen survivor (CUT row rl of the group tile, Doppler d), one lane per
 // cell; it keeps every cell that can detect.  With E(s) = #{fl(s * ref) >= cut}, the cell can
 // only detect if E(s) < need for the scale s it gets.  E(s_min) >= need rules every scale out.
@@ -590,10 +429,7 @@ __device__ __forceinline__ uint32_t wave_select_kth(uint32_t ka, uint32_t kb, ui
   return 0u;  // unreachable for k < #active
 }
 
-#ifndef FMCW_CFAR2D_TWO_STAGE  // phase A as shared-key stage 1 + compacted per-CUT stage 2 (1)
-#define FMCW_CFAR2D_TWO_STAGE 1
-#endif
-template <int NC, int HD, int GD, int TWO = FMCW_CFAR2D_TWO_STAGE>
+template <int NC, int HD, int GD>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
 k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int frame0, int tile0, Cfar2DArgs a,
          DetSink sink) {
@@ -705,26 +541,7 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
         d = (le % TPR) * 16 + (int)(e & 15u);
       };
       const bool tested = has_tile && r >= a.hr && r < ns - a.hr;
-      if constexpr (HD > 0 && FMCW_CFAR2D_SCREEN == 2 && TWO) {
-        // stage 1: one shared key per half lane; stage 2: the per-CUT screen for the blocks (a
-        // lane's 16 cells) stage 1 could not reject entirely, the workgroup's blocks listed and
-        // split over all 256 lanes (L lanes per block take its window rows in turn)
-        const uint32_t s1 = tested ? cfar2d_screen_shared<NC, HD, GD>(rr, rlw, d0, a, need) : 0u;
-        aux[threadIdx.x] = 0u;
-        coop_rounds(s1 ? 1u : 0u, cnt + 12, list, nullptr, 0u, [&](int n) {
-          const int L = n <= 32 ? 8 : n <= 64 ? 4 : n <= 128 ? 2 : 1;
-          const int j = (int)threadIdx.x / L, sub = (int)threadIdx.x % L;
-          if (j < n) {  // whole aligned groups of L lanes
-            int trow, d;
-            const uint32_t e = list[j];
-            cell_of(e, trow, d);
-            const uint32_t b = cfar2d_screen16_split<NC, HD, GD>(rr, trow, d, a, need, sub, L);
-            if (sub == 0) aux[e >> 4] = b;
-          }
-        });
-        cand = s1 ? aux[threadIdx.x] : 0u;
-        __syncthreads();  // every lane has its bits before aux is reused
-      } else if (tested) {
+      if (tested) {
         if constexpr (HD > 0) {
           if constexpr (FMCW_CFAR2D_SCREEN == 2) cand = cfar2d_screen16<NC, HD, GD>(rr, rlw, d0, a, need);
           else if constexpr (FMCW_CFAR2D_SCREEN) cand = cfar2d_screen<NC, HD, GD>(rr, rlw, d0, a, need);

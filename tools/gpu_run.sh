@@ -67,6 +67,11 @@ for s in "$@"; do
     pmc3_fetch) run pmc3_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc3_fetch" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
     pmc3_write) run pmc3_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc3_write" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
     pmc3_sq) run pmc3_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_ACTIVE_INST_ANY -d "$OUT/pmc3_sq" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
+    k3lab) run k3lab_c5 300 tools/k3_lab 16 5 ;;
+    lib_c5)  # config 5 with a variant library (LIB=var_x) at chunk sizes CHUNKS
+      for c in ${CHUNKS:-0 12}; do
+        FMCW_LIB="$PWD/fpga-fmcw-radar-processor_amd/lib/${LIB}.so" run "bench_c5_${LIB}_chunk$c" 300 python bench.py --workload c5 --steps 10 --warmup 3 --no-cpu-baseline --no-h2d --chunk "$c"
+      done ;;
     k1lab)  # K1 variants stand-alone (tools/k1_lab, built on the CPU host): configs 5, 3, 2048
       run k1lab_c5_3f 120 tools/k1_lab 8192 1024 1 3 1 &&
       run k1lab_c5_12f 120 tools/k1_lab 8192 1024 1 12 1 &&

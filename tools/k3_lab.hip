@@ -83,8 +83,7 @@ int main(int argc, char** argv) {
   const int nf = argc > 1 ? std::atoi(argv[1]) : 16;
   const int reps = argc > 2 ? std::atoi(argv[2]) : 5;
   const int ns = argc > 3 ? std::atoi(argv[3]) : 8192;
-  std::vector<Var> vars = {{"k_cfar2d one-stage screen", k_cfar2d<NC, 6, 2, 0>},
-                           {"k_cfar2d two-stage screen", k_cfar2d<NC, 6, 2, 1>}};
+  std::vector<Var> vars = {{"k_cfar2d (production)", k_cfar2d<NC, 6, 2>}};
 #ifdef K3_LAB_VARIANTS
   K3_LAB_VARIANTS
 #endif
