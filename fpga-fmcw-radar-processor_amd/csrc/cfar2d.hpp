@@ -1,29 +1,28 @@
 // cfar2d.hpp -- K3: 2-D OS-CFAR (rtl/src/os_cfar_2d.vhd:140-217) over the linear magnitude
 // map, for gfx950.  Included from inside namespace fmcw by kernels.hpp (uses DetSink,
-// det_reserve_wave, wave_excl_scan, lt_bit, opaque, the magnitude-row format midx / moff /
-// mrow_floats / load_cells and DopplerGeom declared there).
+// det_reserve_wave, wave_excl_scan, lt_bit, opaque, nonneg / q17, MH and DopplerGeom declared
+// there).
 //
 // Tiles.  The detection unit is K2's wave tile: WR = 1024/NC range rows x NC Doppler cells
 // (16 cells per lane), so the 1-D and 2-D CFAR share one sink layout and one (frame, range,
-// doppler) order.  A workgroup (4 waves) takes 4 consecutive wave tiles of one frame and
-// stages their rows plus +-hr halo rows in LDS once, in the magnitude-row format (16-cell
-// circular Doppler halos, 4 pad floats per 16 cells).  After that the waves run on their own.
-// Doppler is circular; a CUT row is tested only if its whole range extent lies inside the map
-// (build spec).
+// doppler) order.  A workgroup (4 waves) takes 4 consecutive wave tiles of one frame (a step)
+// and walks a strip of such steps through a ring of staged rows (the TR rows of the step plus
+// +-hr halo rows).  Doppler is circular; a CUT row is tested only if its whole range extent
+// lies inside the map (build spec).
 //
-// Phase A (every cell, one lane per 16 consecutive cells): for each of the 2 hr + 1 window
-// rows the lane reads that row's 16 + 2 hd span once (16-B LDS reads), scales it by s_min,
-// and counts for each of its 16 CUTs the refs with fl(s_min * ref) < cut (guard rows skip
-// |dd| <= gd).  #{fl(s_min * ref) >= cut} >= n_ref - k proves cut <= fl(s * ranked) for
-// every admissible scale s >= s_min, so such a cell cannot detect; the others are candidates.
-// Phase B (candidates, one whole wave per cell, in cell order): lanes hold refs l and l + 64
-// (fixed order: dr outer, dd inner); the mean is the fixed fp32 halving tree (one add, then
-// xor-shuffles 32..1 == oracle tree_sum_f32); the scale bracket comes from ballot counts
-// (ranked > M <=> #{ref > M} >= n_ref - k; ranked < M' <=> #{ref < M'} >= k + 1); detect <=>
-// #{fl(s * ref) >= cut} < n_ref - k.  Pass 1 decides and counts, the wave reserves its sink
-// range, pass 2 walks its detections again and finds the exact ranked value by a 32-step radix
-// select over order-preserving keys (threshold = fl(s * ranked), dbg_threshold).  No per-cell
-// list is kept, so LDS holds only the rows.
+// Three stages, each conservative (it never drops a cell that can detect), the last exact:
+//  1. Screen (every cell, one lane per 16 consecutive cells), on 7-bit PAIR-MAX keys staged in
+//     LDS: 4 CUTs per 32-bit VALU op (cfar2d_screen7).
+//  2. Candidate test of the screen's survivors (~1.3 % of noise cells), L lanes per cell, on the
+//     exact fp32 cells of the map in global memory (L2 / MALL-resident: the rows were staged
+//     moments before): exact E(s) counts and a bound on the mean (cfar2d_exact_a).
+//  3. Phase B (the candidates, one whole wave per cell, in cell order): lanes hold refs l and
+//     l + 64 (fixed order: dr outer, dd inner); the mean is the fixed fp32 halving tree (one
+//     add, then xor-shuffles 32..1 == oracle tree_sum_f32); the scale bracket comes from ballot
+//     counts (ranked > M <=> #{ref > M} >= n_ref - k; ranked < M' <=> #{ref < M'} >= k + 1);
+//     detect <=> #{fl(s * ref) >= cut} < n_ref - k.  Pass 1 decides and counts, the wave
+//     reserves its sink range, pass 2 walks its detections again and finds the exact ranked
+//     value by a pivoting select (threshold = fl(s * ranked), dbg_threshold).
 #pragma once
 
 struct Cfar2DArgs {
@@ -34,312 +33,240 @@ struct Cfar2DArgs {
   int compat;          // FMCW_COMPAT_CFAR: 17-bit integer cells, integer mean and brackets
 };
 
+// 7-bit keys.  key(v) = clamp((bits(v) >> SH) - base, 0, 127) for a non-negative fp32 cell v:
+// 2^(23 - SH) levels per octave (16 at SH = 19) over a 128-level window that starts `base`
+// levels up; base is set per strip from the mean level of its first step's cells minus LOW
+// (FMCW_K3_KEY_LOW, 64: the window spans 4 octaves below the mean level to 4 above, where
+// Rayleigh noise and the cut / s_min levels it is tested against lie).  The key is monotone
+// non-decreasing in v, with clamping at both ends, and NaN maps to 0 (a NaN reference never
+// counts), so key(ref) > key(q) implies ref > q.  Cells above the window all get 127: they
+// count as references, and as CUTs they are never screened out (no key is above 127).
+#ifndef FMCW_K3_KEY_SHIFT
+#define FMCW_K3_KEY_SHIFT 19
+#endif
+#ifndef FMCW_K3_KEY_LOW
+#define FMCW_K3_KEY_LOW 64
+#endif
+__device__ __forceinline__ uint32_t key7(float v, int base) {
+  const uint32_t b = __float_as_uint(v);
+  const int k = b > 0x7f800000u ? -1 : (int)(b >> FMCW_K3_KEY_SHIFT) - base;
+  return (uint32_t)min(max(k, 0), 127);
+}
+// key(q) + 1 for q = fl(c * inv_s) + 8 ulps (c * fl(1 / s): <= 2 ulps of error), c = the CUT:
+// a pair max whose key is >= this has max > q > c / s in reals, so fl(s * max) >= c.
+// (No NaN test: a NaN cut gets 128, which no key reaches, so the cell is never screened out.)
+__device__ __forceinline__ uint32_t cut_key7(float c, float inv_s, int base) {
+  const int k = (int)((__float_as_uint(c * inv_s) + 8u) >> FMCW_K3_KEY_SHIFT) - base;
+  return (uint32_t)min(max(k, 0), 127) + 1u;
+}
+
+// 16-bit keys (the candidate test's): the high half of the bit pattern of a non-negative cell
+// (sign 0, 8 exponent and 7 mantissa bits), NaN -> 0; lo(k) = float(k << 16) <= cell <=
+// hi(k) = float(k << 16 | 0xffff).
+__device__ __forceinline__ uint32_t key16(float v) {
+  const uint32_t b = __float_as_uint(v);
+  return b > 0x7f800000u ? 0u : b >> 16;
+}
+__device__ __forceinline__ float key_lo(uint32_t k) { return __uint_as_float(k << 16); }
+__device__ __forceinline__ float key_hi(uint32_t k) {  // the inf key bounds as +inf
+  return __uint_as_float(min((k << 16) | 0xffffu, 0x7f800000u));
+}
+// (key16 + 1) of q = fl(c * inv_s) + 8 ulps: a reference whose key16 is strictly above key(q)
+// has ref > q > c / s in reals, so fl(s * ref) >= c.  Clamped so that a packed 16-bit
+// difference never wraps.
+__device__ __forceinline__ uint32_t cut_key16(float c, float inv_s) {
+  return min((__float_as_uint(c * inv_s) + 8u) >> 16, 0x7fffu) + 1u;
+}
+// LDS key16 row: cell d (-MH <= d < NC + MH, circular halos) at k16idx(d), unpadded (the
+// candidate test's reads are scattered anyway; the LDS budget keeps 3 workgroups per CU).
+__host__ __device__ constexpr int k16idx(int d) { return d + MH; }
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// LDS byte row: the pair-max key of cell d (-MH <= d < NC + MH, circular halos) at byte
+// b7idx(d), with bit 7 set: pm(d) = max(key(d), key(d + 1)) | 0x80.  A lane's 32-byte window
+// (cells d0 - 8 .. d0 + 23) is two aligned 16-B reads.
+__host__ __device__ constexpr int b7idx(int d) { return d + MH + 8; }
+
 template <int NC> struct Cfar2DGeom {
   static constexpr int NT = 256;
   static constexpr int WPB = 4;                   // wave tiles per workgroup tile
   static constexpr int WR = DopplerGeom<NC>::WR;  // CUT rows per wave tile
   static constexpr int TR = WPB * WR;             // CUT rows per workgroup tile
-  static constexpr int RS = mrow_floats<NC>();    // LDS row stride (floats)
+  static constexpr int RB = NC + 2 * MH + 16;     // LDS pair-max row stride (bytes)
+  static constexpr int KRS = NC + 2 * MH;        // LDS key16 row stride (keys)
   static constexpr int TPR = NC / 16;             // lanes per row
+  static_assert(RB % 16 == 0 && KRS % 8 == 0 && MH >= 8, "rows stay 16-B aligned; the window is inside the halos");
 };
 
-// The staged rows of one step: a ring of nr = TR + 2 hr rows of rs floats.  Tile row x (0 = the
-// first halo row of the current step) lives in slot (x + base) mod nr, so a strip of steps
-// keeps the 2 hr rows it shares with the next step and loads only TR new ones.
+// The staged rows of one step: a ring of nr = TR + 2 hr slots, each a pair-max byte row (rs
+// bytes) and a key16 row (ks keys).  Tile row x (0 = the first halo row of the current step)
+// lives in slot (x + base) mod nr, so a strip of steps keeps the 2 hr rows it shares with the
+// next step and loads only TR new ones.
 struct RowRing {
-  float* tile;
-  int base, nr, rs;
+  uint8_t* tile;
+  uint16_t* keys;
+  int base, nr, rs, ks;
   __device__ __forceinline__ int slot(int x) const {
     const int y = x + base;
     return y >= nr ? y - nr : y;
   }
-  __device__ __forceinline__ float* row(int x) const { return tile + slot(x) * rs; }
+  __device__ __forceinline__ uint8_t* row(int x) const { return tile + slot(x) * rs; }
+  __device__ __forceinline__ uint16_t* krow(int x) const { return keys + slot(x) * ks; }
 };
 
-__device__ __forceinline__ uint32_t f2key(float f) {
-  const uint32_t u = __float_as_uint(f);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ __forceinline__ float key2f(uint32_t k) {
-  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
-}
-
-#ifndef FMCW_CFAR2D_SCREEN  // phase A: packed 16-bit pair screen (2), fp32 pair screen (1), exact (0);
-#define FMCW_CFAR2D_SCREEN 2  // the screens are followed by the exact count of their survivors
-#endif
-#ifndef FMCW_CFAR2D_PREFETCH  // load a strip's next rows during the current step (1)
-#define FMCW_CFAR2D_PREFETCH 1
-#endif
 constexpr int kCfar2dList = 2 * 256 + 16;  // u32 after the rows: round list, verdicts / positions, counts
 
 template <int NC>
 constexpr size_t cfar2d_smem_bytes(int hr) {
   using G = Cfar2DGeom<NC>;
-  return (size_t)(G::TR + 2 * hr) * G::RS * 4 + kCfar2dList * 4;
+  return (size_t)(G::TR + 2 * hr) * (G::RB + 2 * G::KRS) + kCfar2dList * 4;
 }
 
-// Phase A screen (compile-time HD / GD): disjoint PAIRS of Doppler-adjacent references.  A pair
-// with fl(s_min * min) >= cut holds 2 references with fl(s_min * ref) >= cut (fl(s x) is
-// monotone), so 2 * #{such pairs} is a lower bound on the exact count and a cell whose bound
-// reaches n_ref - k cannot detect.  A reference row of 2 HD + 1 cells gives HD pairs (its last
-// cell is left out), a guard row two segments of HD - GD cells, (HD - GD) / 2 pairs each.
-// On noise + targets about 5 % of the cells pass (0.6 % pass the exact count) at half the
-// compares; the survivors are then counted exactly, one per lane.
+// Screen (compile-time HD <= 8 / GD) over disjoint PAIRS of Doppler-adjacent references: a pair
+// whose max key is >= cut_key7 holds at least one reference with fl(s_min * ref) >= cut, so
+// #{such pairs} is a lower bound on E(s_min) = #{fl(s_min * ref) >= cut}, and a cell whose bound
+// reaches need = n_ref - k cannot detect at any admissible scale.  (The max bound beats 2 x
+// #{pairs whose min qualifies} where it matters: for a reference exceeding the cut's level with
+// probability p it rejects from p ~ 0.32 instead of p ~ 0.52.)  A reference row of 2 HD + 1
+// cells gives HD pairs (its last cell is left out), a guard row two segments of HD - GD cells,
+// (HD - GD) / 2 pairs each.  Four CUTs per dword: Y[p] holds the cut keys of CUTs 4p..4p+3 in
+// its bytes, X the four pair-max bytes (bit 7 set) at the same offset from each, and bit 7 of
+// each byte of X - Y is set iff that pair counts (no byte borrows: X >= 128 > Y - 1); the
+// per-CUT counts (<= 60 < 256) accumulate in the bytes of acc[p] as (t >> 7) & 0x01010101.
+// Per window row: two 16-B LDS reads, <= 6 v_alignbyte for the unaligned X, and 4 VALU per 4
+// (CUT, pair) tests.
 template <int NC, int HD, int GD>
-__device__ __forceinline__ uint32_t cfar2d_screen(const RowRing& rr, int rl, int d0, const Cfar2DArgs& a,
-                                                  int need) {
-  static_assert(HD <= MH, "the window stays inside the row halos");
-  constexpr int W = 16 + 2 * HD;
-  constexpr int O0 = floor4(-HD);
-  constexpr int NV = (W + (-HD - O0) + 3) / 4;
-  constexpr int SEG = HD - GD, NPS = SEG / 2;   // guard-row segment length, pairs per segment
-  const float* lb = rr.row(rl + a.hr) + midx(d0);
-  uint32_t cb[16], nlt[16];  // cut bits; #{pairs with fl(s_min * min) < cut}
-  {
-    float c[16];
-    load_cells<4>(lb, 0, c);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      cb[i] = __float_as_uint(c[i]);
-      nlt[i] = 0;
-    }
-  }
-  for (int dr = -a.hr; dr <= a.hr; ++dr) {
-    float v[4 * NV];
-    load_cells<NV>(rr.row(rl + a.hr + dr) + midx(d0), O0, v);
-    uint32_t pm[W - 1];  // pm[k] = fl(s_min * min(cell k, cell k + 1)), cell 0 = d0 - HD
-#pragma unroll
-    for (int k = 0; k < W - 1; ++k)
-      pm[k] = __float_as_uint(a.s_min * fminf(v[-HD - O0 + k], v[-HD - O0 + k + 1]));
-    if (dr >= -a.gr && dr <= a.gr) {  // guard row (uniform branch)
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-#pragma unroll
-        for (int j = 0; j < NPS; ++j)
-          nlt[i] += lt_bit(pm[i + 2 * j], cb[i]) + lt_bit(pm[i + HD + GD + 1 + 2 * j], cb[i]);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-#pragma unroll
-        for (int j = 0; j < HD; ++j) nlt[i] += lt_bit(pm[i + 2 * j], cb[i]);
-    }
-  }
-  const int n_guard = 2 * a.gr + 1;
-  const int np = (2 * a.hr + 1 - n_guard) * HD + n_guard * 2 * NPS;  // pairs per cell
-  uint32_t bits = 0;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) bits |= (2 * (np - (int)nlt[i]) < need ? 1u : 0u) << i;
-  return bits;
-}
-
-// Phase A screen on packed 16-bit keys, two CUTs per VALU op, over disjoint PAIRS of
-// Doppler-adjacent references.  A pair whose MAX satisfies fl(s_min * max) >= cut holds at
-// least one reference that does, so #{such pairs} is a lower bound on the exact count
-// E(s_min) = #{fl(s_min * ref) >= cut}; a cell whose bound reaches n_ref - k cannot detect at
-// any admissible scale.  (The max bound beats 2 * #{pairs whose min qualifies} exactly where it
-// matters: for a reference exceeding the cut's level with probability p it rejects from
-// p ~ 0.32 instead of p ~ 0.52; on single-channel Rayleigh maps 1.9 % of the cells survive it
-// instead of 4.8 %.)  A reference row of 2 HD + 1 cells gives HD pairs (its last cell is left
-// out), a guard row two segments of HD - GD cells, (HD - GD) / 2 pairs each.
-// The key of a cell is the high half of its bit pattern (cells are non-negative: sign 0, 8
-// exponent and 7 mantissa bits), monotone in the value, so max() commutes with it.  Each CUT
-// gets the key of q = fl(cut / s_min) + 8 ulps (cut * fl(1 / s_min): <= 2 ulps of error), and
-// a pair counts only if its max key is STRICTLY above that key: then max > q > cut / s_min in
-// reals, so s_min * max > cut and fl(s_min * max) >= cut (the key's 2^-7 resolution only makes
-// the screen a little weaker).  Per window row: 27 byte-perms build hi16 pairs, 26
-// v_pk_max_u16 the packed pair maxima, and each (two CUTs, one pair) step is v_pk_sub_u16 +
-// v_pk_lshrrev_b16 + v_pk_add_u16 (bit 15 of pairmax - (key + 1) is set iff pairmax <= key).
-// The survivors are then counted exactly, one per lane.
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-
-template <int NC, int HD, int GD>
-__device__ __forceinline__ uint32_t cfar2d_screen16(const RowRing& rr, int rl, int d0, const Cfar2DArgs& a,
-                                                    int need) {
-  static_assert(HD <= MH, "the window stays inside the row halos");
-  constexpr int W = 16 + 2 * HD;
-  constexpr int O0 = floor4(-HD);
-  constexpr int NV = (W + (-HD - O0) + 3) / 4;
+__device__ __forceinline__ uint32_t cfar2d_screen7(const RowRing& rr, int rl, int d0, const Cfar2DArgs& a,
+                                                   int need, const uint32_t (&Y)[4]) {
+  static_assert(HD >= 1 && HD <= 8, "the window is inside the two 16-B reads");
   constexpr int SEG = HD - GD, NPS = SEG / 2;
-  const float* lb = rr.row(rl + a.hr) + midx(d0);
-  const float inv_s = 1.0f / a.s_min;
-  u16x2 ck[8], nlt[8];  // (key + 1) of CUTs 2p, 2p + 1; #{pairs not counted}
-  {
-    float c[16];
-    load_cells<4>(lb, 0, c);
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      const uint32_t k0 = min((__float_as_uint(c[2 * p] * inv_s) + 8u) >> 16, 0x7fffu) + 1u;
-      const uint32_t k1 = min((__float_as_uint(c[2 * p + 1] * inv_s) + 8u) >> 16, 0x7fffu) + 1u;
-      ck[p] = __builtin_bit_cast(u16x2, k0 | (k1 << 16));
-      nlt[p] = (u16x2)(0);
-    }
-  }
+  constexpr int B0 = 8 - HD;  // byte of cell d0 - HD in the window
+  uint32_t acc[4] = {0u, 0u, 0u, 0u};
   for (int dr = -a.hr; dr <= a.hr; ++dr) {
-    float v[4 * NV];
-    load_cells<NV>(rr.row(rl + a.hr + dr) + midx(d0), O0, v);
-    u16x2 P[W - 2];  // P[k] = (pairmax key k, pairmax key k + 1), cell 0 = d0 - HD
+    const uint8_t* rp = rr.row(rl + a.hr + dr) + b7idx(d0 - 8);
+    uint32_t D[8];  // D[j] = pair-max bytes of cells d0 - 8 + 4j .. + 3
     {
-      uint32_t V[W - 1];  // V[k] = (key of cell k, key of cell k + 1)
-#pragma unroll
-      for (int k = 0; k < W - 1; ++k)
-        V[k] = __builtin_amdgcn_perm(__float_as_uint(v[-HD - O0 + k + 1]), __float_as_uint(v[-HD - O0 + k]),
-                                     0x07060302u);
-#pragma unroll
-      for (int k = 0; k < W - 2; ++k)
-        P[k] = __builtin_elementwise_max(__builtin_bit_cast(u16x2, V[k]), __builtin_bit_cast(u16x2, V[k + 1]));
+      const uint4 q0 = *reinterpret_cast<const uint4*>(rp), q1 = *reinterpret_cast<const uint4*>(rp + 16);
+      D[0] = q0.x; D[1] = q0.y; D[2] = q0.z; D[3] = q0.w;
+      D[4] = q1.x; D[5] = q1.y; D[6] = q1.z; D[7] = q1.w;
     }
+    auto X = [&](int b) -> uint32_t {  // bytes b .. b + 3 of the window (b compile-time after unrolling)
+      return (b & 3) ? __builtin_amdgcn_alignbyte(D[(b >> 2) + 1], D[b >> 2], (uint32_t)(b & 3)) : D[b >> 2];
+    };
+    auto count = [&](int p, uint32_t x) { acc[p] += ((x - Y[p]) >> 7) & 0x01010101u; };
     if (dr >= -a.gr && dr <= a.gr) {  // guard row (uniform branch)
 #pragma unroll
-      for (int p = 0; p < 8; ++p)
+      for (int p = 0; p < 4; ++p)
 #pragma unroll
         for (int j = 0; j < NPS; ++j) {
-          nlt[p] += (u16x2)(P[2 * p + 2 * j] - ck[p]) >> (unsigned short)15;
-          nlt[p] += (u16x2)(P[2 * p + HD + GD + 1 + 2 * j] - ck[p]) >> (unsigned short)15;
+          count(p, X(B0 + 4 * p + 2 * j));
+          count(p, X(B0 + 4 * p + HD + GD + 1 + 2 * j));
         }
     } else {
 #pragma unroll
-      for (int p = 0; p < 8; ++p)
+      for (int p = 0; p < 4; ++p)
 #pragma unroll
-        for (int j = 0; j < HD; ++j) nlt[p] += (u16x2)(P[2 * p + 2 * j] - ck[p]) >> (unsigned short)15;
+        for (int j = 0; j < HD; ++j) count(p, X(B0 + 4 * p + 2 * j));
     }
   }
-  const int n_guard = 2 * a.gr + 1;
-  const int np = (2 * a.hr + 1 - n_guard) * HD + n_guard * 2 * NPS;  // pairs per cell
   uint32_t bits = 0;
 #pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    bits |= (np - (int)nlt[p].x < need ? 1u : 0u) << (2 * p);
-    bits |= (np - (int)nlt[p].y < need ? 1u : 0u) << (2 * p + 1);
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bits |= (((acc[p] >> (8 * q)) & 0xffu) < (uint32_t)need ? 1u : 0u) << (4 * p + q);
+  return bits;
+}
+
+// Screen, runtime geometry (any window the LDS budget allows; Doppler wraps explicitly): the
+// same pair bound, one byte read per (CUT, pair).
+template <int NC>
+__device__ __forceinline__ uint32_t cfar2d_screen7_generic(const RowRing& rr, int rl, int d0, const Cfar2DArgs& a,
+                                                           int need, const uint32_t (&Y)[4]) {
+  const int nps = (a.hd - a.gd) / 2;
+  uint32_t bits = 0;
+  for (int i = 0; i < 16; ++i) {
+    const int d = d0 + i;
+    const uint32_t y = (Y[i >> 2] >> (8 * (i & 3))) & 0xffu;
+    int n = 0;
+    auto pm = [&](const uint8_t* row, int c) { return (uint32_t)row[b7idx(c & (NC - 1))] >= y + 128u ? 1 : 0; };
+    for (int dr = -a.hr; dr <= a.hr; ++dr) {
+      const uint8_t* row = rr.row(rl + a.hr + dr);
+      if (dr >= -a.gr && dr <= a.gr) {
+        for (int j = 0; j < nps; ++j) n += pm(row, d - a.hd + 2 * j) + pm(row, d + a.gd + 1 + 2 * j);
+      } else {
+        for (int j = 0; j < a.hd; ++j) n += pm(row, d - a.hd + 2 * j);
+      }
+    }
+    bits |= (n < need ? 1u : 0u) << i;
   }
   return bits;
 }
 
-// Candidate test of one screen survivor (CUT row rl of the group tile, Doppler d), one lane per
-// cell; it keeps every cell that can detect.  With E(s) = #{fl(s * ref) >= cut}, the cell can
-// only detect if E(s) < need for the scale s it gets.  E(s_min) >= need rules every scale out.
-// The scale is sc_min only when #{ref < mean / 2} >= rank + 1 (os_cfar_2d.vhd:195-199);
-// otherwise it is >= s2 = min(sc_nom, sc_max) and E(s2) >= need rules the cell out too.
-// E(s_min) and E(s2) are bounded from below with the screen's 16-bit keys, both in one packed
-// op per reference (a reference counts if its key is strictly above key(cut / s) + 8 ulps), and
-// #{ref < mean / 2} from above with an any-order fp32 sum x (1 + 2^-15) (the sum of <= 128
-// non-negative terms in another order differs by < 2^-16 relative; compat's integer sums are
-// exact).  On single-channel (Rayleigh) maps this leaves ~0.3 % of the cells E(s_min) alone
-// would pass.  Addresses: midx(d + dd) with a runtime d.
+// Candidate test of one screen survivor (CUT row rl of the group tile, Doppler d; `cut` = the
+// cut or an upper bound of it, here hi(key16): every bound below holds with it, since the
+// references counted lie above cut / s and the half-mean test compares the same value), by L
+// adjacent lanes that split the window rows; it keeps every cell that can
+// detect.  With E(s) = #{fl(s * ref) >= cut}, the cell can only detect if E(s) < need for the
+// scale s it gets.  E(s_min) >= need rules every scale out.  The scale is sc_min only when
+// #{ref < mean / 2} >= rank + 1 (os_cfar_2d.vhd:195-199); otherwise it is >= s2 =
+// min(sc_nom, sc_max) and E(s2) >= need rules the cell out too.  On the key16 rows: E(s_min)
+// and E(s2) are bounded from below (a reference counts if its key is >= cut_key16; E(s2) and
+// the rest only for the ~1/4 of the survivors E(s_min) does not rule out), the mean from above by an any-order fp32 sum of hi(key) x (1 + 2^-15)
+// (<= 128 non-negative terms: any order is within 2^-16 relative; compat's floor(sum / n) >> 1
+// is below the real half), and #{ref < mean / 2} from above by #{lo(key) < half_up}.
+// Compile-time HD: the window is inside the row halos; HD == 0 (runtime geometry): Doppler
+// wraps explicitly.
 template <int NC, int HD, int GD>
-__device__ __forceinline__ bool cfar2d_exact_a(const RowRing& rr, int rl, int d, const Cfar2DArgs& a, int need,
-                                               int sub, int L) {
-  const float* crow = rr.row(rl + a.hr);
-  const int x = d + MH;
-  auto at = [&](const float* row, int dd) { return row[(x + dd) + (((x + dd) >> 4) << 2)]; };
-  const float cut = at(crow, 0);
+__device__ __forceinline__ bool cfar2d_exact_a(const RowRing& rr, int rl, float cut, int d, const Cfar2DArgs& a,
+                                               int need, int sub, int L) {
   const float s2 = a.override_ ? a.s_min : fminf(a.sc_nom, a.sc_max);
-  const uint32_t k1 = min((__float_as_uint(cut * (1.0f / a.s_min)) + 8u) >> 16, 0x7fffu) + 1u;
-  const uint32_t k2 = min((__float_as_uint(cut * (1.0f / s2)) + 8u) >> 16, 0x7fffu) + 1u;
-  const u16x2 kk = __builtin_bit_cast(u16x2, k1 | (k2 << 16));
-  u16x2 nlt = (u16x2)(0);  // #{refs not counted} for (s_min, s2)
-  float sum = 0.f;
+  const uint32_t k1 = cut_key16(cut, 1.0f / a.s_min);
+  const uint32_t k2 = cut_key16(cut, 1.0f / s2);
   auto visit = [&](auto&& fn) {  // this lane's rows: dr = -hr + sub, every L-th
     for (int dr = -a.hr + sub; dr <= a.hr; dr += L) {
-      const float* row = rr.row(rl + a.hr + dr);
-      if (dr >= -a.gr && dr <= a.gr) {
+      const uint16_t* row = rr.krow(rl + a.hr + dr);
+      const bool grow = dr >= -a.gr && dr <= a.gr;
+      if constexpr (HD > 0) {
+        if (grow) {
 #pragma unroll
-        for (int dd = -HD; dd <= HD; ++dd)
-          if (dd < -GD || dd > GD) fn(at(row, dd));
+          for (int dd = -HD; dd <= HD; ++dd)
+            if (dd < -GD || dd > GD) fn((uint32_t)row[k16idx(d + dd)]);
+        } else {
+#pragma unroll
+          for (int dd = -HD; dd <= HD; ++dd) fn((uint32_t)row[k16idx(d + dd)]);
+        }
       } else {
-#pragma unroll
-        for (int dd = -HD; dd <= HD; ++dd) fn(at(row, dd));
+        for (int dd = -a.hd; dd <= a.hd; ++dd)
+          if (!grow || dd < -a.gd || dd > a.gd) fn((uint32_t)row[k16idx((d + dd) & (NC - 1))]);
       }
     }
   };
-  visit([&](float v) {
-    const uint32_t kv = __builtin_amdgcn_perm(__float_as_uint(v), __float_as_uint(v), 0x07060302u);
-    nlt += (u16x2)(__builtin_bit_cast(u16x2, kv) - kk) >> (unsigned short)15;
-    sum += v;
+  // pass 1 (most survivors end here): #{refs not counted} at s_min
+  int n1 = 0;
+  visit([&](uint32_t kv) { n1 += kv < k1 ? 1 : 0; });
+  for (int x = 1; x < L; x <<= 1) n1 += __shfl_xor(n1, x, 64);  // the cell's L lanes are adjacent and aligned
+  if (a.n_ref - n1 >= need) return false;                         // E(s_min) >= need
+  // pass 2: the same at s2, and the mean bound
+  int n2 = 0;
+  float sum = 0.f;
+  visit([&](uint32_t kv) {
+    n2 += kv < k2 ? 1 : 0;
+    sum += key_hi(kv);
   });
-  for (int x = 1; x < L; x <<= 1) {  // the cell's L lanes are adjacent and aligned
-    nlt += __builtin_bit_cast(u16x2, __shfl_xor(__builtin_bit_cast(int, nlt), x, 64));
+  for (int x = 1; x < L; x <<= 1) {
+    n2 += __shfl_xor(n2, x, 64);
     sum += __shfl_xor(sum, x, 64);
   }
-  if (a.n_ref - (int)nlt.x >= need) return false;                // E(s_min) >= need
-  if (a.n_ref - (int)nlt.y < need || a.override_) return true;   // E(s2) may be < need
+  if (a.n_ref - n2 < need || a.override_) return true;            // E(s2) may be < need
   const float half_up = sum * (1.0f + 1.0f / 32768.0f) / (float)a.n_ref * 0.5f;
-  // >= need refs lie above cut / s2; if cut / s2 >= mean / 2 they all lie above the half, so
+  // >= need refs lie above cut / s2; if that is >= mean / 2 they all lie above the half, so
   // n_lo <= n_ref - need = rank < rank + 1 without counting (most noise survivors: their cut
   // is high).  (1 - 2^-20) covers the product's rounding.
   if (cut * (1.0f / s2) * (1.0f - 1.0f / 1048576.0f) >= half_up) return false;
   int n_lo = 0;
-  visit([&](float v) { n_lo += v < half_up ? 1 : 0; });
+  visit([&](uint32_t kv) { n_lo += key_lo(kv) < half_up ? 1 : 0; });
   for (int x = 1; x < L; x <<= 1) n_lo += __shfl_xor(n_lo, x, 64);
   return n_lo >= a.rank + 1;                                     // sc_min still possible
-}
-
-// Phase A for a compile-time Doppler extent HD / guard GD; returns this lane's candidate bits.
-// `rl` is the CUT row within the workgroup tile (tile row rl + hr).
-template <int NC, int HD, int GD>
-__device__ __forceinline__ uint32_t cfar2d_phase_a(const RowRing& rr, int rl, int d0, const Cfar2DArgs& a,
-                                                   int need) {
-  static_assert(HD <= MH, "the window stays inside the row halos");
-  constexpr int W = 16 + 2 * HD;
-  constexpr int O0 = floor4(-HD);
-  constexpr int NV = (W + (-HD - O0) + 3) / 4;
-  const float* lb = rr.row(rl + a.hr) + midx(d0);
-  uint32_t cb[16], lt[16];   // cut bits; #{fl(s_min * ref) < cut} (lt_bit: no SGPR masks)
-  {
-    float c[16];
-    load_cells<4>(lb, 0, c);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      cb[i] = __float_as_uint(c[i]);
-      lt[i] = 0;
-    }
-  }
-  for (int dr = -a.hr; dr <= a.hr; ++dr) {
-    float v[4 * NV];
-    load_cells<NV>(rr.row(rl + a.hr + dr) + midx(d0), O0, v);
-    uint32_t sb[W];
-#pragma unroll
-    for (int k = 0; k < W; ++k) sb[k] = __float_as_uint(a.s_min * v[-HD - O0 + k]);
-    if (dr >= -a.gr && dr <= a.gr) {  // guard row: skip |dd| <= GD (uniform branch)
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-#pragma unroll
-        for (int dd = -HD; dd <= HD; ++dd)
-          if (dd < -GD || dd > GD) lt[i] += lt_bit(sb[i + HD + dd], cb[i]);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-#pragma unroll
-        for (int dd = -HD; dd <= HD; ++dd) lt[i] += lt_bit(sb[i + HD + dd], cb[i]);
-    }
-  }
-  // candidate <=> #{fl(s_min * ref) >= cut} < need  <=>  lt > n_ref - need
-  uint32_t bits = 0;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) bits |= ((int)lt[i] > a.n_ref - need ? 1u : 0u) << i;
-  return bits;
-}
-
-// Phase A, runtime geometry (any window the LDS budget allows; Doppler wraps explicitly).
-template <int NC>
-__device__ __forceinline__ uint32_t cfar2d_phase_a_generic(const RowRing& rr, int rl, int d0,
-                                                           const Cfar2DArgs& a, int need) {
-  const float* crow = rr.row(rl + a.hr);
-  uint32_t bits = 0;
-  for (int i = 0; i < 16; ++i) {
-    const int d = d0 + i;
-    const uint32_t c = __float_as_uint(crow[midx(d)]);
-    uint32_t lt = 0;
-    for (int dr = -a.hr; dr <= a.hr; ++dr) {
-      const float* row = rr.row(rl + a.hr + dr);
-      const bool grow = dr >= -a.gr && dr <= a.gr;
-      for (int dd = -a.hd; dd <= a.hd; ++dd) {
-        if (grow && dd >= -a.gd && dd <= a.gd) continue;
-        lt += lt_bit(__float_as_uint(a.s_min * row[midx((d + dd) & (NC - 1))]), c);
-      }
-    }
-    bits |= ((int)lt > a.n_ref - need ? 1u : 0u) << i;
-  }
-  return bits;
 }
 
 // Reference j of the fixed order (dr ascending outer, dd ascending inner, guard block
@@ -429,15 +356,18 @@ __device__ __forceinline__ uint32_t wave_select_kth(uint32_t ka, uint32_t kb, ui
   return 0u;  // unreachable for k < #active
 }
 
+#ifndef FMCW_K3_WAVES  // waves per SIMD the register budget is cut for
+#define FMCW_K3_WAVES 4
+#endif
 template <int NC, int HD, int GD>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FMCW_K3_WAVES)))
 k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int frame0, int tile0, Cfar2DArgs a,
          DetSink sink) {
   using Gm = Cfar2DGeom<NC>;
-  constexpr int WR = Gm::WR, NT = Gm::NT, RS = Gm::RS, TPR = Gm::TPR, WPB = Gm::WPB, TR = Gm::TR;
+  constexpr int WR = Gm::WR, NT = Gm::NT, RB = Gm::RB, TPR = Gm::TPR, WPB = Gm::WPB, TR = Gm::TR;
   static_assert(TR * NC == 4 * 4 * NT, "a step's new rows are 4 float4 per thread");
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* const tile = smem;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem8[];
+  uint8_t* const tile = smem8;
 
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -452,18 +382,32 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
   const int spf = (wg_per_frame + steps - 1) / steps;    // strips per frame
   const int nf = n_strips / spf;
   const int nr = TR + 2 * a.hr;                          // ring rows
-  uint32_t* const list = reinterpret_cast<uint32_t*>(tile + nr * RS);
+  uint16_t* const keys = reinterpret_cast<uint16_t*>(tile + nr * RB);
+  uint32_t* const list = reinterpret_cast<uint32_t*>(keys + nr * Gm::KRS);
   uint32_t* const aux = list + kCoopRound;
   uint32_t* const cnt = aux + kCoopRound;
   const int tid = opaque(threadIdx.x);
 
-  // one float4 of cells (row x, Doppler d..d+3) into the ring, with its circular-halo copy
-  auto put4 = [&](const RowRing& rr, int x, int d, float4 v) {
+  // one float4 of cells (row x, Doppler d..d+3) plus the cell d+4 after it (circularly) into
+  // the ring as 4 pair-max key bytes, with its circular-halo copy
+  auto put4 = [&](const RowRing& rr, int x, int d, float4 v, float v4, int kb) {
     v = a.compat ? q17x4(v) : nonneg4(v);
-    float* row = rr.row(x);
-    *reinterpret_cast<float4*>(row + midx(d)) = v;
-    if (d < MH) *reinterpret_cast<float4*>(row + midx(NC + d)) = v;
-    if (d >= NC - MH) *reinterpret_cast<float4*>(row + midx(d - NC)) = v;
+    v4 = a.compat ? q17(v4) : nonneg(v4);
+    const uint32_t k0 = key7(v.x, kb), k1 = key7(v.y, kb), k2 = key7(v.z, kb), k3 = key7(v.w, kb), k4 = key7(v4, kb);
+    const uint32_t w = max(k0, k1) | (max(k1, k2) << 8) | (max(k2, k3) << 16) | (max(k3, k4) << 24) | 0x80808080u;
+    const uint2 kw = make_uint2(key16(v.x) | (key16(v.y) << 16), key16(v.z) | (key16(v.w) << 16));
+    uint8_t* row = rr.row(x);
+    uint16_t* krow = rr.krow(x);
+    *reinterpret_cast<uint32_t*>(row + b7idx(d)) = w;
+    *reinterpret_cast<uint2*>(krow + k16idx(d)) = kw;
+    if (d < MH) {
+      *reinterpret_cast<uint32_t*>(row + b7idx(NC + d)) = w;
+      *reinterpret_cast<uint2*>(krow + k16idx(NC + d)) = kw;
+    }
+    if (d >= NC - MH) {
+      *reinterpret_cast<uint32_t*>(row + b7idx(d - NC)) = w;
+      *reinterpret_cast<uint2*>(krow + k16idx(d - NC)) = kw;
+    }
   };
 
   for (int g = blockIdx.x; g < n_strips; g += gridDim.x) {
@@ -472,31 +416,76 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
     const int f = g % nf;
     const int t_beg = (g / nf) * steps, t_end = min(t_beg + steps, wg_per_frame);
     const float* fm = map + (size_t)f * ns * NC;
-    RowRing rr{tile, 0, nr, RS};
+    // an exact cell of the frame (as staged: clamped at 0, or 17-bit integer in compat mode)
+    auto cell = [&](int r, int d) {
+      const float v = fm[(size_t)r * NC + d];
+      return a.compat ? q17(v) : nonneg(v);
+    };
+    RowRing rr{tile, keys, 0, nr, RB, Gm::KRS};
     float4 pre[4];
+    float pre4[4];
+    // the strip's key base: mean level of the first step's CUT rows minus FMCW_K3_KEY_LOW
+    int kb;
+    {
+      uint32_t s = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e4 = tid + u * NT;
+        const int i = e4 / (NC / 4), d = (e4 - i * (NC / 4)) * 4;
+        const int rs = min(t_beg * TR + i, ns - 1);
+        float4 v = *reinterpret_cast<const float4*>(fm + (size_t)rs * NC + d);
+        v = a.compat ? q17x4(v) : nonneg4(v);
+        s += (min(__float_as_uint(v.x), 0x7f800000u) >> FMCW_K3_KEY_SHIFT) +
+             (min(__float_as_uint(v.y), 0x7f800000u) >> FMCW_K3_KEY_SHIFT) +
+             (min(__float_as_uint(v.z), 0x7f800000u) >> FMCW_K3_KEY_SHIFT) +
+             (min(__float_as_uint(v.w), 0x7f800000u) >> FMCW_K3_KEY_SHIFT);
+      }
+#pragma unroll
+      for (int x = 32; x >= 1; x >>= 1) s += (uint32_t)__shfl_xor((int)s, x, 64);
+      __syncthreads();  // the previous strip is done with cnt
+      if (threadIdx.x == 0) cnt[12] = 0u;
+      __syncthreads();
+      if (lane == 0) atomicAdd(&cnt[12], s);
+      __syncthreads();
+      kb = (int)(cnt[12] / (uint32_t)(TR * NC)) - FMCW_K3_KEY_LOW;
+    }
     for (int t = t_beg; t < t_end; ++t) {
       const int wt0 = t * WPB;                             // first wave tile of this step
       const int n_wt = min(WPB, wt_per_frame - wt0);
       const int r0 = wt0 * WR;                             // first CUT row of this step
+      // this lane's 16 CUT cells (row r0 + rlw, Doppler d0..d0+15), loaded before the staging so
+      // that their latency hides behind it
+      const int rlw = wv * WR + lane / TPR;    // CUT row within the group tile
+      const int d0 = (lane % TPR) * 16;
+      const int r = r0 + rlw;
+      float4 cuts[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        cuts[p] = *reinterpret_cast<const float4*>(fm + (size_t)min(r, ns - 1) * NC + d0 + 4 * p);
       __syncthreads();  // the previous step's waves are done with the rows and the lists
       if (t == t_beg) {
         // rows r0-hr .. r0+TR+hr-1 (zero outside the map), 4 float4 loads in flight per lane
         const int n4 = nr * (NC / 4);
         for (int b = tid; b < n4; b += 4 * NT) {
           float4 v[4];
+          float v4[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int e4 = b + u * NT;
             const int x = e4 / (NC / 4), d = (e4 - x * (NC / 4)) * 4;
             const int r = r0 - a.hr + x;
             v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (e4 < n4 && r >= 0 && r < ns) v[u] = *reinterpret_cast<const float4*>(fm + (size_t)r * NC + d);
+            v4[u] = 0.f;
+            if (e4 < n4 && r >= 0 && r < ns) {
+              v[u] = *reinterpret_cast<const float4*>(fm + (size_t)r * NC + d);
+              v4[u] = fm[(size_t)r * NC + ((d + 4) & (NC - 1))];
+            }
           }
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int e4 = b + u * NT;
             const int x = e4 / (NC / 4), d = (e4 - x * (NC / 4)) * 4;
-            if (e4 < n4) put4(rr, x, d, v[u]);
+            if (e4 < n4) put4(rr, x, d, v[u], v4[u], kb);
           }
         }
       } else {
@@ -508,31 +497,27 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
         for (int u = 0; u < 4; ++u) {
           const int e4 = tid + u * NT;
           const int i = e4 / (NC / 4), d = (e4 - i * (NC / 4)) * 4;
-          if (!FMCW_CFAR2D_PREFETCH) {
-            const int rn = r0 + a.hr + i;  // new row of this step (zero past the map)
-            pre[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (rn < ns) pre[u] = *reinterpret_cast<const float4*>(fm + (size_t)rn * NC + d);
-          }
-          put4(rr, nr - TR + i, d, pre[u]);
+          put4(rr, nr - TR + i, d, pre[u], pre4[u], kb);
         }
       }
-      if (FMCW_CFAR2D_PREFETCH && t + 1 < t_end) {  // prefetch the next step's new rows r0 + TR + hr ..
+      if (t + 1 < t_end) {  // prefetch the next step's new rows r0 + TR + hr .. (zero past the map)
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int e4 = tid + u * NT;
           const int i = e4 / (NC / 4), d = (e4 - i * (NC / 4)) * 4;
           const int r = r0 + TR + a.hr + i;
           pre[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (r < ns) pre[u] = *reinterpret_cast<const float4*>(fm + (size_t)r * NC + d);
+          pre4[u] = 0.f;
+          if (r < ns) {
+            pre[u] = *reinterpret_cast<const float4*>(fm + (size_t)r * NC + d);
+            pre4[u] = fm[(size_t)r * NC + ((d + 4) & (NC - 1))];
+          }
         }
       }
       __syncthreads();
       const bool has_tile = wv < n_wt;  // uniform per wave; waves without a tile still join the barriers
 
       // ---- Phase A: candidates among this lane's 16 cells
-      const int rlw = wv * WR + lane / TPR;    // CUT row within the group tile
-      const int d0 = (lane % TPR) * 16;
-      const int r = r0 + rlw;
       uint32_t cand = 0;
       // cell of a round-list entry (wave << 10 | lane << 4 | bit) -> group-tile row, Doppler bin
       auto cell_of = [&](uint32_t e, int& trow, int& d) {
@@ -542,24 +527,33 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
       };
       const bool tested = has_tile && r >= a.hr && r < ns - a.hr;
       if (tested) {
-        if constexpr (HD > 0) {
-          if constexpr (FMCW_CFAR2D_SCREEN == 2) cand = cfar2d_screen16<NC, HD, GD>(rr, rlw, d0, a, need);
-          else if constexpr (FMCW_CFAR2D_SCREEN) cand = cfar2d_screen<NC, HD, GD>(rr, rlw, d0, a, need);
-          else cand = cfar2d_phase_a<NC, HD, GD>(rr, rlw, d0, a, need);
-        } else {
-          cand = cfar2d_phase_a_generic<NC>(rr, rlw, d0, a, need);
+        uint32_t Y[4];  // cut_key7 of this lane's 16 CUTs, 4 per dword
+        const float inv_s = 1.0f / a.s_min;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const float4 c = a.compat ? q17x4(cuts[p]) : nonneg4(cuts[p]);
+          Y[p] = cut_key7(c.x, inv_s, kb) | (cut_key7(c.y, inv_s, kb) << 8) | (cut_key7(c.z, inv_s, kb) << 16) |
+                 (cut_key7(c.w, inv_s, kb) << 24);
         }
-      }
-#ifdef FMCW_CFAR2D_ABLATE
-      if (FMCW_CFAR2D_ABLATE != 4)
+        if constexpr (HD > 0) cand = cfar2d_screen7<NC, HD, GD>(rr, rlw, d0, a, need, Y);
+        else cand = cfar2d_screen7_generic<NC>(rr, rlw, d0, a, need, Y);
+#ifdef FMCW_K3_ABLATE  // timing experiments (tools/k3_lab): 3 = staging + cut keys only, 1 = + screen
+        if (FMCW_K3_ABLATE == 3) cand = Y[0] == 12345u ? 1u : 0u;
+        if (FMCW_K3_ABLATE == 1) cand = cand == 0xffffu ? 1u : 0u;
 #endif
-      if constexpr (HD > 0 && FMCW_CFAR2D_SCREEN) {
+      }
+      uint32_t n_cand = 1u;  // candidates in the workgroup's step (nonzero: phase B runs)
+#ifdef FMCW_K3_ABLATE  // 5 = no candidate test (phase B takes every screen survivor)
+      if (FMCW_K3_ABLATE != 5)
+#endif
+      {
         // survivors of the screen -> candidate test, 256 per round over the whole workgroup (a
         // hot tile's survivors spread over all four waves).  A round of <= 32 / 64 / 128 cells
         // gives each cell 8 / 4 / 2 adjacent lanes that split its rows: a step usually has a
         // few dozen survivors, and one lane walking all 128 references of a cell alone set the
-        // critical path of the step (config 5: 89 -> 71 us per frame).
+        // critical path of the step.
         aux[threadIdx.x] = 0u;
+        if (threadIdx.x == 0) cnt[13] = 0u;  // candidates of the step (read after the rounds' barriers)
         const uint32_t scr = cand;
         coop_rounds(scr, cnt, list, nullptr, 0u, [&](int n) {
           const int L = n <= 32 ? 8 : n <= 64 ? 4 : n <= 128 ? 2 : 1;
@@ -568,19 +562,54 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
             int trow, d;
             const uint32_t e = list[j];
             cell_of(e, trow, d);
-            if (cfar2d_exact_a<NC, HD, GD>(rr, trow, d, a, need, sub, L) && sub == 0)
+#ifdef FMCW_K3_ABLATE  // 4 = the candidate test's rounds without the test
+            if (FMCW_K3_ABLATE == 4) {
+              if (e == 0xffffffffu) atomicOr(&aux[0], 1u);
+            } else
+#endif
+            if (cfar2d_exact_a<NC, HD, GD>(rr, trow, key_hi(rr.krow(trow + a.hr)[k16idx(d)]), d, a, need, sub, L) &&
+                sub == 0)
+            {
               atomicOr(&aux[e >> 4], 1u << (e & 15u));
+              atomicAdd(&cnt[13], 1u);
+            }
           }
         });
         cand = aux[threadIdx.x];
-        __syncthreads();  // every lane has its bits before aux is cleared again
+        n_cand = cnt[13];
+        __syncthreads();  // every lane has its bits (and the count) before aux / cnt[13] change
+#ifdef FMCW_K3_COUNT  // tools/k3_lab: screen survivors and candidates into sink.counter[2], [3]
+        {
+          int s1 = __popc(scr), s2 = __popc(cand);
+          for (int o = 32; o >= 1; o >>= 1) {
+            s1 += __shfl_xor(s1, o, 64);
+            s2 += __shfl_xor(s2, o, 64);
+          }
+          if (lane == 0) {
+            atomicAdd(&sink.counter[2], (uint32_t)s1);
+            atomicAdd(&sink.counter[3], (uint32_t)s2);
+          }
+        }
+#endif
+      }
+#ifdef FMCW_K3_ABLATE  // 2 = + candidate test, no phase B
+      if (FMCW_K3_ABLATE == 2) n_cand = 0u;
+#endif
+      const int wtile = tile0 + f * wt_per_frame + wt0 + wv;
+      if (n_cand == 0u) {  // (most steps) no candidate: the tiles are empty, phase B's barriers skipped
+        if (has_tile && lane == 0) {
+          sink.wg_base[wtile] = (uint32_t)wtile * sink.slot_cap;
+          sink.wg_count[wtile] = 0u;
+        }
+        continue;
       }
 
-      // ---- Phase B: one whole wave per candidate cell.  Lanes hold refs l and l + 64 of the fixed
-      // order; the mean is the fixed fp32 halving tree; the scale bracket comes from ballot counts.
+      // ---- Phase B: one whole wave per candidate cell, on the exact fp32 cells of the map.
+      // Lanes hold refs l and l + 64 of the fixed order; the mean is the fixed fp32 halving
+      // tree; the scale bracket comes from ballot counts.
       auto refs_of = [&](int trow, int d, float& va, float& vb) {
-        va = oka ? rr.row(trow + a.hr + dra)[midx((d + dda) & (NC - 1))] : 0.f;
-        vb = okb ? rr.row(trow + a.hr + drb)[midx((d + ddb) & (NC - 1))] : 0.f;
+        va = oka ? cell(r0 + trow + dra, (d + dda) & (NC - 1)) : 0.f;
+        vb = okb ? cell(r0 + trow + drb, (d + ddb) & (NC - 1)) : 0.f;
       };
       auto scale_of = [&](float va, float vb) -> float {
         float sum = va + vb;
@@ -603,9 +632,6 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
         const int n_lo = __popcll(__ballot(oka && va < half)) + __popcll(__ballot(okb && vb < half));
         return (n_hi >= need) ? a.sc_max : (n_lo >= a.rank + 1) ? a.sc_min : a.sc_nom;
       };
-#ifdef FMCW_CFAR2D_ABLATE  // timing experiments only: 1 = no phase B, 2 = no ranked-value select
-      if (FMCW_CFAR2D_ABLATE == 1) cand = 0;
-#endif
 
       // Pass 1: decide every candidate; the four waves take the round's entries in turn
       aux[threadIdx.x] = 0u;
@@ -614,21 +640,17 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
           int trow, d;
           const uint32_t e = list[j];
           cell_of(e, trow, d);
-          const float cut = rr.row(trow + a.hr)[midx(d)];
+          const float cut = cell(r0 + trow, d);
           float va, vb;
           refs_of(trow, d, va, vb);
           const float sc = scale_of(va, vb);
           const int n_ge = __popcll(__ballot(oka && sc * va >= cut)) + __popcll(__ballot(okb && sc * vb >= cut));
-#ifdef FMCW_CFAR2D_ABLATE  // 3 / 4: every candidate / screen survivor is reported (counting)
-          if (FMCW_CFAR2D_ABLATE >= 3 && lane == 0) atomicOr(&aux[e >> 4], 1u << (e & 15u));
-#endif
           if (n_ge < need && lane == 0) atomicOr(&aux[e >> 4], 1u << (e & 15u));
         }
       });
       const uint32_t detw = aux[threadIdx.x];
       int total;
       const int dx = wave_excl_scan(__popc(detw), total);
-      const int wtile = tile0 + f * wt_per_frame + wt0 + wv;
       const uint32_t base = has_tile ? det_reserve_wave(sink, wtile, total) : 0u;
       __syncthreads();  // aux now carries sink positions
 
@@ -642,18 +664,14 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
           float va, vb;
           refs_of(trow, d, va, vb);
           const float sc = scale_of(va, vb);
-          uint32_t ranked = 0;
-#ifdef FMCW_CFAR2D_ABLATE
-          if (FMCW_CFAR2D_ABLATE != 2)
-#endif
-          ranked = wave_select_kth(oka ? __float_as_uint(va) : 0u, okb ? __float_as_uint(vb) : 0u,
-                                   __ballot(oka), __ballot(okb), a.rank);
+          const uint32_t ranked = wave_select_kth(oka ? __float_as_uint(va) : 0u, okb ? __float_as_uint(vb) : 0u,
+                                                  __ballot(oka), __ballot(okb), a.rank);
           if (lane == 0 && slot < sink.cap) {
             fmcw_det dd;
             dd.frame = (uint32_t)(frame0 + f);
             dd.range = (uint16_t)(r0 + trow);
             dd.doppler = (uint16_t)d;
-            dd.mag = rr.row(trow + a.hr)[midx(d)];
+            dd.mag = cell(r0 + trow, d);
             dd.threshold = sc * __uint_as_float(ranked);
             sink.scratch[slot] = dd;
           }

@@ -68,6 +68,8 @@ for s in "$@"; do
     pmc3_write) run pmc3_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc3_write" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
     pmc3_sq) run pmc3_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_ACTIVE_INST_ANY -d "$OUT/pmc3_sq" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
     k3lab) run k3lab_c5 300 tools/k3_lab 16 5 ;;
+    k3labs)  # every tools/k3_lab_<variant> binary (built on the CPU host with other -D switches)
+      for b in tools/k3_lab_*; do run "k3lab_c5_${b#tools/k3_lab_}" 300 "$b" 16 5; done ;;
     lib_c5)  # config 5 with a variant library (LIB=var_x) at chunk sizes CHUNKS
       for c in ${CHUNKS:-0 12}; do
         FMCW_LIB="$PWD/fpga-fmcw-radar-processor_amd/lib/${LIB}.so" run "bench_c5_${LIB}_chunk$c" 300 python bench.py --workload c5 --steps 10 --warmup 3 --no-cpu-baseline --no-h2d --chunk "$c"
