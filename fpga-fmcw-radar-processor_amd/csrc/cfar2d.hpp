@@ -357,7 +357,7 @@ __device__ __forceinline__ uint32_t wave_select_kth(uint32_t ka, uint32_t kb, ui
 }
 
 #ifndef FMCW_K3_WAVES  // waves per SIMD the register budget is cut for
-#define FMCW_K3_WAVES 4
+#define FMCW_K3_WAVES 3
 #endif
 template <int NC, int HD, int GD>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FMCW_K3_WAVES)))
