@@ -131,6 +131,7 @@ __device__ __forceinline__ int opaque(int x) {
 typedef float fmcw_f4v __attribute__((ext_vector_type(4)));
 typedef float fmcw_f2v __attribute__((ext_vector_type(2)));
 typedef uint32_t fmcw_u2v __attribute__((ext_vector_type(2)));
+typedef uint32_t fmcw_u4v __attribute__((ext_vector_type(4)));
 template <bool NT>
 __device__ __forceinline__ float4 ld_f4(const void* p) {
   fmcw_f4v v;

@@ -160,7 +160,7 @@ struct fmcw_handle {
   int n_cu = 256;
   // range kernel geometry (runtime copies of RangeGeom<N>)
   int T = 0, RB = 0, lgT = 0, lgRB = 0;
-  int k1_want = kRangeSeq;  // preferred K1 family (environment FMCW_K1 at fmcw_create)
+  int k1_want = kRangePx;   // preferred K1 family (environment FMCW_K1 at fmcw_create)
   int k1_kind = kRangeSingle;  // the family the handle runs
   bool k2_fast = false;    // K2 runs its FAST instantiation (fixed at fmcw_create)
   uint32_t chunk = 1;
@@ -263,7 +263,7 @@ int validate(const fmcw_config& c) {
     return fail(FMCW_EINVAL, "map_kind=%d unknown", c.map_kind);
   if (c.mti_mode != FMCW_MTI_OFF && c.mti_mode != FMCW_MTI_2PULSE && c.mti_mode != FMCW_MTI_3PULSE)
     return fail(FMCW_EINVAL, "mti_mode=%d unknown (0 off, 2 or 3 pulse)", c.mti_mode);
-  if (range_info(c.n_range, c.in_dtype, c.window, false, kRangeSeq).T > (int)c.n_doppler)
+  if (range_info(c.n_range, c.in_dtype, c.window, false, kRangePx).T > (int)c.n_doppler)
     return fail(FMCW_EINVAL, "n_doppler=%u smaller than the range kernel's chirp group", c.n_doppler);
   if (c.max_frames < 1) return fail(FMCW_EINVAL, "max_frames must be >= 1");
   if (c.cfar_kind == FMCW_CFAR_OS1D) {
@@ -586,10 +586,11 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   h->cfg = *cfg;
   const fmcw_config& c = h->cfg;
   h->n_cu = prop.multiProcessorCount;
-  // K1 family: the sequential-pair kernel where instantiated (N = 4096, 8192), else the dual
-  // one (N >= 2048), else k_range; environment FMCW_K1=single|dual|seq caps it (A/B runs)
+  // K1 family: k_range_px at N = 8192, the sequential-pair kernel at N = 4096, else the dual
+  // one (N >= 2048), else k_range; environment FMCW_K1=single|dual|seq|px caps it (A/B runs)
   if (const char* k1 = std::getenv("FMCW_K1"))
-    h->k1_want = !std::strcmp(k1, "single") ? kRangeSingle : !std::strcmp(k1, "dual") ? kRangeDual : kRangeSeq;
+    h->k1_want = !std::strcmp(k1, "single") ? kRangeSingle : !std::strcmp(k1, "dual") ? kRangeDual
+               : !std::strcmp(k1, "seq") ? kRangeSeq : kRangePx;
   h->k2_fast = k2_fast(c);
   const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, c.spectrum_dtype == FMCW_SPEC_F16, h->k1_want);
   h->k1_kind = ri.kind;

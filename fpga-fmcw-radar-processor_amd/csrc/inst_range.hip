@@ -49,12 +49,24 @@ RangeInfo range_sq(int dtype) {
   return {fn, SqGeom<N, S::V>::T, SqGeom<N, S::V>::RB, NT, kRangeSeq};
 }
 
+// k_range_px (round 3): N = 8192, two LDS exchanges + a permlane radix-2 (kernels.hpp)
+RangeInfo range_px(int dtype) {
+  RangeFn fn = nullptr;
+  switch (dtype) {
+    case FMCW_IN_F32: fn = k_range_px<LoadF32>; break;
+    case FMCW_IN_F16: fn = k_range_px<LoadF16>; break;
+    case FMCW_IN_I16: fn = k_range_px<LoadI16>; break;
+  }
+  return {fn, 2, 64, 512, kRangePx};
+}
+
 }  // namespace
 
 RangeInfo range_info(uint32_t n, int dtype, int window, bool h16, int want) {
   const bool q15 = window == FMCW_WIN_Q15_RTL;
   // the dual / sequential-pair kernels: fp32 window, fp32 spectrum
   if (!q15 && !h16) {
+    if (want >= kRangePx && FMCW_K1_PX && n == 8192) return range_px(dtype);
     if (want >= kRangeSeq && FMCW_K1_SQ && n >= (uint32_t)FMCW_K1_SQ) {
       switch (n) {
         case 4096: return range_sq<4096>(dtype);

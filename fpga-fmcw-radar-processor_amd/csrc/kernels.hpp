@@ -70,6 +70,7 @@ struct LoadF32 {
     return ld_f2<FMCW_NT_CUBE>(reinterpret_cast<const float2*>(base) + idx);
   }
   __device__ __forceinline__ static float2 expand1(Raw1 r) { return r; }
+  __device__ __forceinline__ static float2 expand1_scaled(Raw1 r, float s) { return make_float2(r.x * s, r.y * s); }
 };
 struct LoadF16 {
   static constexpr int bytes = 4;
@@ -92,6 +93,14 @@ struct LoadF16 {
     const h2 h = __builtin_bit_cast(h2, u);
     return make_float2((float)h[0], (float)h[1]);
   }
+  // (I, Q) * s: v_fma_mix_f32 converts the half and multiplies in one instruction (fma(x, s, 0) =
+  // fl(x s): the fp16 -> fp32 conversion is exact)
+  __device__ __forceinline__ static float2 expand1_scaled(Raw1 u, float s) {
+    float re, im;
+    asm("v_fma_mix_f32 %0, %1, %2, 0 op_sel_hi:[1,0,0]" : "=v"(re) : "v"(u), "v"(s));
+    asm("v_fma_mix_f32 %0, %1, %2, 0 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(im) : "v"(u), "v"(s));
+    return make_float2(re, im);
+  }
 };
 struct LoadI16 {
   static constexpr int bytes = 4;
@@ -113,6 +122,10 @@ struct LoadI16 {
     typedef short s2 __attribute__((ext_vector_type(2)));
     const s2 s = __builtin_bit_cast(s2, u);
     return make_float2((float)s[0], (float)s[1]);
+  }
+  __device__ __forceinline__ static float2 expand1_scaled(Raw1 u, float w) {
+    const float2 x = expand1(u);
+    return make_float2(x.x * w, x.y * w);
   }
 };
 
@@ -556,6 +569,171 @@ k_range_sq(const void* __restrict__ cube, float2* __restrict__ inter, const floa
         const int d = t + P * gg + LL * m;
         const size_t off = fbase + ((size_t)(d / RB) * ncb + cb) * (RB * T) + (size_t)(d % RB) * T;
         st_f4<FMCW_NT_SPEC_ST>(inter + off, make_float4(X[0][gg][m].x, X[0][gg][m].y, X[1][gg][m].x, X[1][gg][m].y));
+      }
+  }
+}
+
+// --------------------------------------------------------------------------------------
+// K1 "permlane pair" k_range_px<LD> for N = 8192 (round 3): k_range_sq's sequential pair with
+// 16 values per thread (512 threads, one 68 KiB transform buffer, two workgroups per CU), but
+// 8192 = 16 x 16 x 16 x 2 with two LDS exchanges instead of three:
+//   pass A  radix 16 from registers (one fp16/int16/fp32 sample per lane per load, stride 512),
+//           window x Doppler weight fused, written to LDS;
+//   pass B  radix 16 through LDS (sub-transforms 16 -> 256);
+//   pass C  radix 16 read from LDS into registers (256 -> 4096), thread (lane l, wave w) taking
+//           j = (l & 31) + 32 w + 256 (l >> 5): the two half-waves hold the two 4096-point
+//           halves y0, y1 at the same offsets k + 256 m;
+//   pass D  the last radix-2 (4096 -> 8192) between the half-waves: v_permlane32_swap of
+//           registers m and m + 8 leaves each lane 8 complete (y0, y1) pairs, p = k + 256 m',
+//           m' = m + 8 (1 - h), X[p] = y0 + W^p y1, X[p + 4096] = y0 - W^p y1.
+// (Measured and dropped: pass B inside each wave -- lane (w, l) playing pass-A thread u + 32 i and
+// pass-B thread 16 u + i, u = 4 w + (l >> 4), i = l & 15, so the A -> B exchange needs no barrier
+// -- makes every pass-A load instruction read 16-B runs of 16 lines: 132 us per 3-frame launch
+// (105 us with cached loads) against 58 us, profiles/r03/k1px/k1lab_c5_3f_wl.log.)
+// The first chirp's 16 outputs wait in registers while the second is transformed, then both go out
+// as 16-B (chirp 0, chirp 1) tile elements: lanes 0-31 and 32-63 each write 512 contiguous bytes.
+// Replaces the Xilinx range FFT (rtl/src/radar_core.vhd:303-316) + corner turner (:318-327).
+// --------------------------------------------------------------------------------------
+#ifndef FMCW_K1_PX          // k_range_px at N = 8192 (1) or k_range_sq (0)
+#define FMCW_K1_PX 1
+#endif
+__device__ __forceinline__ void swap32(float2& a, float2& b) {
+  // a, b := [a_lo, b_lo], [a_hi, b_hi] (lo / hi = lanes 0-31 / 32-63)
+  const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.x), __float_as_uint(b.x), false, false);
+  const auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.y), __float_as_uint(b.y), false, false);
+  a = make_float2(__uint_as_float(rx[0]), __uint_as_float(ry[0]));
+  b = make_float2(__uint_as_float(rx[1]), __uint_as_float(ry[1]));
+}
+template <typename LD, int W = 4>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(W)))
+k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const float* __restrict__ win,
+           const float* __restrict__ chirp_w, int nc, int n_groups, float /* q15_scale */, uint32_t* /* status */) {
+  constexpr int N = 8192, T = 2, RB = 64;
+  static_assert(RangeGeom<N>::T == T && RangeGeom<N>::RB == RB, "tile format of K2");
+  __shared__ __attribute__((aligned(16))) float2 lds[padded(N)];
+  const int t0 = threadIdx.x;
+  const int lane = t0 & 63, wv = t0 >> 6, h = lane >> 5;
+  const int ncb = nc / T;
+
+  // loads and stores through buffer descriptors: one lane offset, the m-dependent part in the
+  // SGPR offset (no 64-bit address per load / store in VGPRs)
+  using Raw1 = typename LD::Raw1;
+  constexpr int SB = sizeof(Raw1);  // bytes per sample
+  constexpr int NTL = FMCW_NT_CUBE ? 2 : 0;  // non-temporal cube loads (read once)
+  Raw1 a[16];
+  float cwn = 1.f;
+  auto fetch = [&](int g, int q) {
+    const int fr = g / ncb;
+    const int cb = g - fr * ncb;
+    const size_t chirp = (size_t)fr * nc + (size_t)cb * T + q;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(reinterpret_cast<const char*>(cube)) + chirp * N * SB, (short)0, N * SB, 0x00020000);
+    const int vo = opaque(t0) * SB;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      if constexpr (SB == 4) {
+        a[m] = __builtin_bit_cast(Raw1, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, m * 512 * SB, NTL));
+      } else {
+        a[m] = __builtin_bit_cast(Raw1, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, m * 512 * SB, NTL));
+      }
+    }
+    if (chirp_w) cwn = chirp_w[__builtin_amdgcn_readfirstlane(cb * T + q)];
+  };
+  float wh[16];  // range window of samples t + 512 m, held
+#pragma unroll
+  for (int m = 0; m < 16; ++m) wh[m] = win[t0 + 512 * m];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) asm volatile("" ::"v"(wh[i]));  // complete before the loop (vmcnt order)
+
+  // pass C's group j = kc + 256 h; the pass-D twiddle base W_8192^(kc + 2048 (1 - h))
+  const int kc = (lane & 31) + 32 * wv;
+  const float2 cd = twiddle<N>(kc + 2048 * (1 - h));
+
+  int g = blockIdx.x;
+  if (g < n_groups) fetch(g, 0);
+  for (; g < n_groups; g += gridDim.x) {
+    const int fr = g / ncb;
+    const int cb = g - fr * ncb;
+    float2 X[2][16];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int t = opaque(t0);
+      const float cw = cwn;
+      __syncthreads();  // the previous transform's pass-C reads are done with lds
+      {  // pass A: window, radix 16 over x[t + 512 m]
+        float2 v[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) v[m] = LD::expand1_scaled(a[m], wh[m] * cw);
+        Dft<16>::run(v);
+        float2* d = lds + pad16(16 * t);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) d[m] = v[m];
+      }
+      // the next chirp's input: this group's second chirp, or the next group's first
+      if (q == 0) fetch(g, 1);
+      else if (g + (int)gridDim.x < n_groups) fetch(g + gridDim.x, 0);
+      {  // pass B: radix 16, L = 16 (in place, barriers around the exchange)
+        __syncthreads();
+        float2 v[16];
+        const float2* src = lds + pad16(t);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) v[m] = src[padoff(m * 512)];
+        __syncthreads();
+        const int k = t & 15;
+        GroupTwiddles<16, 256> tb;
+        tb.init(k);
+#pragma unroll
+        for (int m = 1; m < 16; ++m) v[m] = cmul(v[m], tb.pow(m));
+        Dft<16>::run(v);
+        float2* dst = lds + pad16((t >> 4) * 256 + k);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) dst[padoff(m * 16)] = v[m];
+        __syncthreads();
+      }
+      {  // pass C: radix 16, L = 256, into registers; v[m] = y_h[kc + 256 m]
+        float2* v = X[q];
+        const float2* src = lds + pad16(opaque(kc + 256 * h));
+#pragma unroll
+        for (int m = 0; m < 16; ++m) v[m] = src[padoff(m * 512)];
+        GroupTwiddles<16, 4096> tc;
+        tc.init(opaque(kc));
+#pragma unroll
+        for (int m = 1; m < 16; ++m) v[m] = cmul(v[m], tc.pow(m));
+        float2 cdl = cd;  // per chirp: the W_32^m products below must not be hoisted (14 VGPRs)
+        asm volatile("" : "+v"(cdl.x), "+v"(cdl.y));
+        Dft<16>::run(v);
+        // pass D: radix 2 between the half-waves; X[q][m + 8] = y0[p], X[q][m] = y1[p] ->
+        // X[q][m + 8] = X[p], X[q][m] = X[p + 4096], p = kc + 256 (m + 8 (1 - h))
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          swap32(v[m + 8], v[m]);
+          // W_8192^(p) = cd * W_32^m
+          const float2 w32 = make_float2(__builtin_cosf(2.0f * 3.14159265358979323846f * m / 32.f),
+                                         -__builtin_sinf(2.0f * 3.14159265358979323846f * m / 32.f));
+          const float2 tw = m ? cmul(cdl, w32) : cdl;
+          const float2 b = cmul(v[m], tw);
+          const float2 a0 = v[m + 8];
+          v[m + 8] = cadd(a0, b);
+          v[m] = csub(a0, b);
+        }
+      }
+    }
+    // tile stores: lane holds X[d] of both chirps for d = p (register m + 8) and p + 4096 (m)
+    // d / 64 = (w >> 1) + 4 m' + 64 s, d % 64 = (l & 31) + 32 (w & 1); tile (d / 64, cb) is 1 KiB
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(inter + (size_t)fr * N * nc, (short)0, N * nc * 8, 0x00020000);
+    const int t = opaque(t0);
+    const int l = t & 63, w = t >> 6;
+    const int vo = (((w >> 1) + 32 * (1 - (l >> 5))) * ncb + cb) * 1024 + ((l & 31) + 32 * (w & 1)) * 16;
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int r = s ? m : m + 8;
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v x = {X[0][r].x, X[0][r].y, X[1][r].x, X[1][r].y};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(fmcw_u4v, x), rs, vo, (4 * m + 64 * s) * ncb * 1024,
+                                               FMCW_NT_SPEC_ST ? 2 : 0);
       }
   }
 }

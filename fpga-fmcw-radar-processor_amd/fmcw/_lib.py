@@ -29,7 +29,7 @@ COMM_ID_BYTES = 128
 K_RANGE, K_DOPPLER, K_CFAR2D, K_COMPACT, K_COUNT = 0, 1, 2, 3, 4
 KERNEL_NAMES = ("k_range", "k_doppler", "k_cfar", "k_compact")
 INFO_CHUNK, INFO_RANGE_KERNEL, INFO_WINDOW_SATURATIONS, INFO_WORD_SATURATIONS = 4, 6, 7, 8
-RANGE_KERNELS = ("k_range", "k_range2", "k_range_sq")   # FMCW_INFO_RANGE_KERNEL values 0, 1, 2
+RANGE_KERNELS = ("k_range", "k_range2", "k_range_sq", "k_range_px")   # FMCW_INFO_RANGE_KERNEL 0..3
 STATUS_WORDS = 4      # FMCW_STATUS_WORDS: n_dets_dev = found, lost, window / word saturations
 
 STATUS_NAMES = {0: "FMCW_OK", -1: "FMCW_EINVAL", -2: "FMCW_ENOMEM", -3: "FMCW_EHIP",

@@ -19,7 +19,7 @@ from test_gpu_parity import check_map, oracle_dets, run_range_ct, to_complex
 
 pytestmark = pytest.mark.gpu
 
-KINDS = {"single": 0, "dual": 1, "seq": 2}
+KINDS = {"single": 0, "dual": 1, "seq": 2, "px": 3}
 
 
 def _run(monkeypatch, kind, **kw):
@@ -39,17 +39,21 @@ def _run(monkeypatch, kind, **kw):
     (2048, 64, 1, "f32", 0),     # below both: every family request falls back to k_range
 ])
 def test_range_kernel_families_agree(monkeypatch, ns, nc, nrx, dtype, mti):
-    """FMCW_K1=single|dual|seq: each family's map is on parity with the oracle (1e-4); where the
-    sequential-pair kernel runs the dual kernel's passes (N = 8192) they are bit-identical, and
-    the detections match the oracle CFAR on each map bit for bit."""
+    """FMCW_K1=single|dual|seq|px: each family's map is on parity with the oracle (1e-4); where the
+    sequential-pair kernel runs the dual kernel's passes (N = 8192) they are bit-identical, the
+    permlane kernel (N = 8192) agrees with them to 1e-5, and the detections match the oracle CFAR
+    on each map bit for bit."""
     nf = 2
     cube = synth.frames(nf, ns, nc, nrx, "two_targets", dtype=dtype, seed=17)
     outs = {}
-    for kind in ("single", "dual", "seq"):
+    for kind in ("single", "dual", "seq", "px"):
         got, out = _run(monkeypatch, kind, cube=cube, N_RANGE=ns, N_DOPPLER=nc, N_RX=nrx, in_dtype=dtype,
                         cfar="os1d", max_frames=nf, mti_bypass=mti == 0, NOTCH_MODE=mti or 2)
-        # k_range2 from N = 4096 (FMCW_K1_DUAL), k_range_sq at 4096 / 8192: below, k_range
+        # k_range2 from N = 4096 (FMCW_K1_DUAL), k_range_sq at 4096 / 8192, k_range_px at 8192
+        # (px asked at 4096 gives k_range_sq): below, k_range
         want = KINDS[kind] if ns >= 4096 else KINDS["single"]
+        if kind == "px" and ns != 8192:
+            want = KINDS["seq"] if ns >= 4096 else KINDS["single"]
         assert got == want, (kind, got)
         outs[kind] = out
     ref = np.stack([O.process(to_complex(cube[f], dtype), None, mti_mode=mti)["mag"] for f in range(nf)])
@@ -59,8 +63,29 @@ def test_range_kernel_families_agree(monkeypatch, ns, nc, nrx, dtype, mti):
     np.testing.assert_array_equal(outs["single"].rd_map, outs["dual"].rd_map)
     if ns == 8192:
         np.testing.assert_array_equal(outs["seq"].rd_map, outs["dual"].rd_map)
+        assert rel_err(outs["px"].rd_map, outs["dual"].rd_map) <= 1e-5
     else:
         assert rel_err(outs["seq"].rd_map, outs["dual"].rd_map) <= 1e-5
+
+
+@pytest.mark.parametrize("dtype", ["f16", "f32", "i16"])
+def test_range_ct_px_many_groups(monkeypatch, dtype):
+    """k_range_px (N = 8192) over many chirp groups per workgroup and an odd group count per
+    launch, every input word type: the canonical corner-turned spectrum vs the oracle, both chirps
+    of every group (the permlane last pass and the half-wave tile stores)."""
+    monkeypatch.setenv("FMCW_K1", "px")
+    ns, nc, nf = 8192, 128, 11     # 704 chirp pairs: more than one per resident workgroup
+    cube = synth.frames(nf, ns, nc, 1, "random_target", dtype=dtype, seed=29)
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, in_dtype=dtype, cfar="none", max_frames=nf) as core:
+        assert core.info("range_kernel") == KINDS["px"]
+        din = DeviceBuffer(cube.nbytes)
+        din.upload(cube)
+        spec = DeviceBuffer(nf * ns * nc * 8)
+        core.range_ct(din, spec, nf)
+        got = spec.download(np.complex64, (nf, 1, ns, nc))
+    for f in range(nf):
+        ref = O.range_ct(to_complex(cube[f], dtype))
+        assert rel_err(got[f], ref) <= 1e-4, f
 
 
 def test_range_ct_seq_many_groups(monkeypatch):
