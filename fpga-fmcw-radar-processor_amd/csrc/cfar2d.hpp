@@ -359,6 +359,7 @@ __device__ __forceinline__ uint32_t wave_select_kth(uint32_t ka, uint32_t kb, ui
 #ifndef FMCW_K3_WAVES  // waves per SIMD the register budget is cut for
 #define FMCW_K3_WAVES 3
 #endif
+
 template <int NC, int HD, int GD>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FMCW_K3_WAVES)))
 k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int frame0, int tile0, Cfar2DArgs a,
@@ -547,14 +548,16 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
       if (FMCW_K3_ABLATE != 5)
 #endif
       {
+        // (Measured and dropped: each wave testing its own survivors without workgroup barriers,
+        // 643 vs 623 us per 16 frames at config 5 -- the rounds balance the waves' survivors.)
         // survivors of the screen -> candidate test, 256 per round over the whole workgroup (a
         // hot tile's survivors spread over all four waves).  A round of <= 32 / 64 / 128 cells
         // gives each cell 8 / 4 / 2 adjacent lanes that split its rows: a step usually has a
         // few dozen survivors, and one lane walking all 128 references of a cell alone set the
         // critical path of the step.
+        const uint32_t scr = cand;
         aux[threadIdx.x] = 0u;
         if (threadIdx.x == 0) cnt[13] = 0u;  // candidates of the step (read after the rounds' barriers)
-        const uint32_t scr = cand;
         coop_rounds(scr, cnt, list, nullptr, 0u, [&](int n) {
           const int L = n <= 32 ? 8 : n <= 64 ? 4 : n <= 128 ? 2 : 1;
           const int j = (int)threadIdx.x / L, sub = (int)threadIdx.x % L;

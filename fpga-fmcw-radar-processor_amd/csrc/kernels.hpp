@@ -604,6 +604,9 @@ __device__ __forceinline__ void swap32(float2& a, float2& b) {
   a = make_float2(__uint_as_float(rx[0]), __uint_as_float(ry[0]));
   b = make_float2(__uint_as_float(rx[1]), __uint_as_float(ry[1]));
 }
+// (Measured and dropped: an XOR-swizzled unpadded layout in which pass A stores into exactly the
+// slots its own lane read in the previous pass C, so the barrier between them goes (3 per chirp):
+// 64.9 vs 59.3 us per 3-frame launch, equal at 12 frames -- profiles/r03/k1px/k1lab_c5_sw.log.)
 template <typename LD, int W = 4>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(W)))
 k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const float* __restrict__ win,

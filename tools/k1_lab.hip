@@ -75,7 +75,6 @@ void add_vars(std::vector<Var>& v) {
   v.push_back({"sq_v32_e2", k_range_sq<N, LD, 32, 2>, N / 32});
   if constexpr (N == 8192) {
     v.push_back({"px", k_range_px<LD>, 512});
-    v.push_back({"px_w3", k_range_px<LD, 3>, 512});
   }
 }
 
