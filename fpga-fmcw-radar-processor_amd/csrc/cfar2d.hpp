@@ -454,15 +454,10 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
       const int wt0 = t * WPB;                             // first wave tile of this step
       const int n_wt = min(WPB, wt_per_frame - wt0);
       const int r0 = wt0 * WR;                             // first CUT row of this step
-      // this lane's 16 CUT cells (row r0 + rlw, Doppler d0..d0+15), loaded before the staging so
-      // that their latency hides behind it
+      // this lane's 16 CUT cells: row r0 + rlw, Doppler d0..d0+15
       const int rlw = wv * WR + lane / TPR;    // CUT row within the group tile
       const int d0 = (lane % TPR) * 16;
       const int r = r0 + rlw;
-      float4 cuts[4];
-#pragma unroll
-      for (int p = 0; p < 4; ++p)
-        cuts[p] = *reinterpret_cast<const float4*>(fm + (size_t)min(r, ns - 1) * NC + d0 + 4 * p);
       __syncthreads();  // the previous step's waves are done with the rows and the lists
       if (t == t_beg) {
         // rows r0-hr .. r0+TR+hr-1 (zero outside the map), 4 float4 loads in flight per lane
@@ -528,13 +523,22 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
       };
       const bool tested = has_tile && r >= a.hr && r < ns - a.hr;
       if (tested) {
-        uint32_t Y[4];  // cut_key7 of this lane's 16 CUTs, 4 per dword
+        // cut_key7 of this lane's 16 CUTs, 4 per dword, from their staged key16 (an upper bound of
+        // the cut, as the candidate test uses: a higher threshold only keeps more cells).  No
+        // global re-read of the CUT cells: with 3 workgroups per CU their rows had often left L2
+        // again (K3 moved 1.8x the map bytes).
+        uint32_t Y[4];
         const float inv_s = 1.0f / a.s_min;
+        {
+          const uint16_t* kr = rr.krow(rlw + a.hr) + k16idx(d0);
+          const uint4 ka = *reinterpret_cast<const uint4*>(kr), kc = *reinterpret_cast<const uint4*>(kr + 8);
+          const uint32_t kw[8] = {ka.x, ka.y, ka.z, ka.w, kc.x, kc.y, kc.z, kc.w};
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          const float4 c = a.compat ? q17x4(cuts[p]) : nonneg4(cuts[p]);
-          Y[p] = cut_key7(c.x, inv_s, kb) | (cut_key7(c.y, inv_s, kb) << 8) | (cut_key7(c.z, inv_s, kb) << 16) |
-                 (cut_key7(c.w, inv_s, kb) << 24);
+          for (int p = 0; p < 4; ++p) {
+            const uint32_t w0 = kw[2 * p], w1 = kw[2 * p + 1];
+            Y[p] = cut_key7(key_hi(w0 & 0xffffu), inv_s, kb) | (cut_key7(key_hi(w0 >> 16), inv_s, kb) << 8) |
+                   (cut_key7(key_hi(w1 & 0xffffu), inv_s, kb) << 16) | (cut_key7(key_hi(w1 >> 16), inv_s, kb) << 24);
+          }
         }
         if constexpr (HD > 0) cand = cfar2d_screen7<NC, HD, GD>(rr, rlw, d0, a, need, Y);
         else cand = cfar2d_screen7_generic<NC>(rr, rlw, d0, a, need, Y);

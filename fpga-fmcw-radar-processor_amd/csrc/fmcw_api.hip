@@ -164,7 +164,6 @@ struct fmcw_handle {
   int k1_kind = kRangeSingle;  // the family the handle runs
   bool k2_fast = false;    // K2 runs its FAST instantiation (fixed at fmcw_create)
   uint32_t chunk = 1;
-  uint32_t chunk_unit = 0;  // auto chunk: frames per K2 grid round; calls split into balanced chunks of it (0: plain)
   // device buffers
   float* win_r = nullptr;  // [ns]
   float* win_d = nullptr;  // [nc]
@@ -552,40 +551,17 @@ void fmcw_config_default(fmcw_config* c) {
 // 96, 0.55 at 108-120, 0.81 from 256 frames up (reads from HBM); K1 unchanged.  Within that,
 // a multiple of the frames one full round of K2's persistent grid covers (config 2: 3072
 // waves / 256 wave tiles = 12 frames, K1 the same), so neither kernel ends on a partial round.
-uint32_t auto_chunk(fmcw_handle* h, size_t frame_inter) {
+uint32_t auto_chunk(const fmcw_handle* h, size_t frame_inter) {
   const fmcw_config& c = h->cfg;
   constexpr size_t kMallBudget = 192u << 20;
   size_t ch = std::max<size_t>(1, kMallBudget / frame_inter);
   const size_t waves = (size_t)h->grid_doppler * (doppler_info(c.n_doppler).NT / 64);
   const size_t tpf = (size_t)c.n_range / doppler_info(c.n_doppler).WR;
-  h->chunk_unit = 1;
   if (waves % tpf == 0) {
     const size_t unit = waves / tpf;  // frames per full K2 round
-    if (ch >= 2 * unit) {
-      ch -= ch % unit;
-      h->chunk_unit = (uint32_t)unit;
-    }
+    if (ch >= 2 * unit) ch -= ch % unit;
   }
   return (uint32_t)std::min<size_t>(c.max_frames, ch);
-}
-
-// Frames of chunk ci of a call over n_frames: plain h->chunk-sized chunks (the last one short)
-// for a caller-set chunk_frames; with the auto chunk the same number of chunks, balanced in whole
-// K2 rounds (chunk_unit frames), so no launch is left with a sliver -- config 5 (3-frame chunks)
-// runs 16 frames as 3,3,3,3,2,2 instead of 3,3,3,3,3,1 (a 1-frame K1 launch is one chirp pair
-// per workgroup: nothing to overlap its loads and stores with).
-void chunk_span(const fmcw_handle* h, size_t n_frames, size_t ci, size_t n_chunks, size_t* f0, size_t* nf) {
-  if (!h->chunk_unit || n_chunks == 1) {
-    *f0 = ci * h->chunk;
-    *nf = std::min<size_t>(h->chunk, n_frames - *f0);
-    return;
-  }
-  const size_t u = h->chunk_unit;
-  const size_t units = (n_frames + u - 1) / u;  // the last unit may be partial
-  const size_t base = units / n_chunks, extra = units % n_chunks;
-  const size_t u0 = ci * base + std::min(ci, extra);
-  *f0 = u0 * u;
-  *nf = std::min(n_frames, (u0 + base + (ci < extra ? 1 : 0)) * u) - *f0;
 }
 
 int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
@@ -644,7 +620,6 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   ALLOC(h->win_d, c.n_doppler * sizeof(float));
   // K1 / K2 address a launch's spectrum with 32-bit byte offsets (buffer loads and stores)
   h->chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(h->chunk, ((size_t)1 << 32) / frame_inter - 1));
-  if (h->chunk_unit > 1 && h->chunk % h->chunk_unit) h->chunk_unit = 1;  // balanced chunks stay <= chunk
   // >= one fp32 frame: fmcw_range_ct writes the fp32 spectrum through it whatever spectrum_dtype
   h->inter_bytes = std::max((size_t)h->chunk * frame_inter, (size_t)c.n_rx * c.n_range * c.n_doppler * sizeof(float2));
   ALLOC(h->inter, h->inter_bytes);
@@ -737,9 +712,11 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
   const size_t n_chunks = (n_frames + h->chunk - 1) / h->chunk;
   size_t k3_f0 = 0;  // first frame of the caller's map not yet through the 2-D CFAR
   for (size_t ci = 0; ci < n_chunks; ++ci) {
-    size_t f0, nfz;
-    chunk_span(h, n_frames, ci, n_chunks, &f0, &nfz);
-    const int nf = (int)nfz;
+    // (Measured and dropped: the same number of chunks balanced in whole K2 rounds -- config 5's
+    // 16 frames as 3,3,3,3,2,2 instead of 3,3,3,3,3,1: K2 59 -> 61 us per launch, configs 3 / 5
+    // 1 % slower, profiles/r03/s2/ab_c*_b*.log.)
+    const size_t f0 = ci * h->chunk;
+    const int nf = (int)std::min<size_t>(h->chunk, n_frames - f0);
     const void* src = static_cast<const char*>(cube) + f0 * in_frame_bytes;
     {
       const int n_groups = nf * (int)c.n_rx * (int)(c.n_doppler / ri.T);

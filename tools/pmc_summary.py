@@ -27,7 +27,7 @@ import re
 PATTERNS = {
     "c2": {"k_range": r"k_range\w*<1024,", "k_doppler": r"k_doppler<256,"},
     "c3": {"k_range": r"k_range\w*<4096,", "k_doppler": r"k_doppler<512,", "k_cfar": r"k_cfar2d<512,"},
-    "c5": {"k_range": r"k_range\w*<8192,", "k_doppler": r"k_doppler<1024,", "k_cfar": r"k_cfar2d<1024,"},
+    "c5": {"k_range": r"k_range(\w*<8192,|_px<)", "k_doppler": r"k_doppler<1024,", "k_cfar": r"k_cfar2d<1024,"},
 }
 ALG = {  # algorithmic bytes per frame, fp32 spectrum
     "c2": {"k_range": 1024 * 256 * 16, "k_doppler": 1024 * 256 * 12},
