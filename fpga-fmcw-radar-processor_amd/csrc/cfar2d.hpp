@@ -211,7 +211,8 @@ __device__ __forceinline__ uint32_t cfar2d_screen7_generic(const RowRing& rr, in
 // #{ref < mean / 2} >= rank + 1 (os_cfar_2d.vhd:195-199); otherwise it is >= s2 =
 // min(sc_nom, sc_max) and E(s2) >= need rules the cell out too.  On the key16 rows: E(s_min)
 // and E(s2) are bounded from below (a reference counts if its key is >= cut_key16; E(s2) and
-// the rest only for the ~1/4 of the survivors E(s_min) does not rule out), the mean from above by an any-order fp32 sum of hi(key) x (1 + 2^-15)
+// the rest decided only for the survivors E(s_min) does not rule out), the mean from above by an
+// any-order fp32 sum of lo(key) x (1 + 2^-7 + 2^-14) + 2^-119
 // (<= 128 non-negative terms: any order is within 2^-16 relative; compat's floor(sum / n) >> 1
 // is below the real half), and #{ref < mean / 2} from above by #{lo(key) < half_up}.
 // Compile-time HD: the window is inside the row halos; HD == 0 (runtime geometry): Doppler
@@ -241,24 +242,27 @@ __device__ __forceinline__ bool cfar2d_exact_a(const RowRing& rr, int rl, float 
       }
     }
   };
-  // pass 1 (most survivors end here): #{refs not counted} at s_min
-  int n1 = 0;
-  visit([&](uint32_t kv) { n1 += kv < k1 ? 1 : 0; });
-  for (int x = 1; x < L; x <<= 1) n1 += __shfl_xor(n1, x, 64);  // the cell's L lanes are adjacent and aligned
-  if (a.n_ref - n1 >= need) return false;                         // E(s_min) >= need
-  // pass 2: the same at s2, and the mean bound
-  int n2 = 0;
+  // one walk: #{refs not counted} at s_min and at s2, and the mean bound.  (Two walks -- the
+  // second only for cells E(s_min) does not rule out -- read every key twice in practice: a
+  // round's wave runs the second walk whenever any of its cells needs it, which is nearly always.)
+  int n1 = 0, n2 = 0;
   float sum = 0.f;
   visit([&](uint32_t kv) {
+    n1 += kv < k1 ? 1 : 0;
     n2 += kv < k2 ? 1 : 0;
-    sum += key_hi(kv);
+    sum += key_lo(kv);  // hi(k) <= lo(k) (1 + 2^-7) for normal keys; the bound below widens by that
   });
-  for (int x = 1; x < L; x <<= 1) {
+  for (int x = 1; x < L; x <<= 1) {  // the cell's L lanes are adjacent and aligned
+    n1 += __shfl_xor(n1, x, 64);
     n2 += __shfl_xor(n2, x, 64);
     sum += __shfl_xor(sum, x, 64);
   }
+  if (a.n_ref - n1 >= need) return false;                         // E(s_min) >= need
   if (a.n_ref - n2 < need || a.override_) return true;            // E(s2) may be < need
-  const float half_up = sum * (1.0f + 1.0f / 32768.0f) / (float)a.n_ref * 0.5f;
+  // upper bound of mean / 2: sum of lo(key) x (1 + 2^-7 + 2^-14) (key precision, then the any-order
+  // fp32 sum of <= 128 non-negative terms, within 2^-16) + 2^-119 (the subnormal keys, where
+  // hi / lo is unbounded: 128 x 2^-126)
+  const float half_up = (sum * (1.0f + 1.0f / 128.0f + 1.0f / 16384.0f) + 0x1p-119f) / (float)a.n_ref * 0.5f;
   // >= need refs lie above cut / s2; if that is >= mean / 2 they all lie above the half, so
   // n_lo <= n_ref - need = rank < rank + 1 without counting (most noise survivors: their cut
   // is high).  (1 - 2^-20) covers the product's rounding.
