@@ -1413,6 +1413,9 @@ __device__ __forceinline__ float2 win_q15c(float2 x, float c, uint32_t& n) {
   return make_float2((float)si, (float)sq);
 }
 
+#ifndef FMCW_K2_SOFF_CHAIN  // K2 prefetch: the SGPR load offsets advanced per load, not hoisted (1)
+#define FMCW_K2_SOFF_CHAIN 1
+#endif
 #ifndef FMCW_K2_PREFETCH  // K2 (MTI off): points of the next (tile, rx) unit loaded ahead (0, 8 or 16)
 #define FMCW_K2_PREFETCH 16
 #endif
@@ -1543,6 +1546,11 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
         if ((P & (T - 1)) == 0) {  // uniform: chirps t + P m sit a fixed S elements apart
           const SE* pb = p + ((((uint32_t)tq >> lgT) << lgRB) << lgT) + ((uint32_t)tq & (uint32_t)(T - 1));
           const uint32_t S = (uint32_t)(P >> lgT) << (lgRB + lgT);
+          // the uniform m S byte offsets, one SGPR advanced per load: left to the compiler, the 16
+          // products were hoisted out of the tile loop and held in 16 SGPRs, which pushed 25
+          // others into VGPR lanes (a v_readlane per use inside the loop)
+          uint32_t so = 0;
+          const uint32_t sb = S * (uint32_t)sizeof(SE);
 #pragma unroll
           for (int m = 0; m < NPF; ++m) {
             if constexpr (!H16 && FMCW_K2_BUFLD) {
@@ -1551,9 +1559,10 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
               const uint32_t vo = (uint32_t)((const char*)pb - (const char*)inter);
               typedef float f2v __attribute__((ext_vector_type(2)));
               const f2v r = __builtin_bit_cast(
-                  f2v, __builtin_amdgcn_raw_buffer_load_b64(srs, vo, (uint32_t)m * S * (uint32_t)sizeof(SE),
-                                                            FMCW_NT_SPEC_LD ? 2 /* nt */ : 0));
+                  f2v, __builtin_amdgcn_raw_buffer_load_b64(srs, vo, so, FMCW_NT_SPEC_LD ? 2 /* nt */ : 0));
               nxt[m] = make_float2(r.x, r.y);
+              so += sb;
+              if constexpr (FMCW_K2_SOFF_CHAIN) asm volatile("" : "+s"(so));
             } else {
               nxt[m] = ld_spec<FMCW_NT_SPEC_LD>(pb + (size_t)m * S, sscale);
             }
