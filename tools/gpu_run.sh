@@ -84,6 +84,11 @@ for s in "$@"; do
       for c in ${CHUNKS:-3 6 12 24}; do
         run "bench_${w}_chunk$c" 300 python bench.py --workload "$w" --frames 24 --steps 6 --warmup 2 --no-cpu-baseline --no-h2d --chunk "$c"
       done ;;
+    chunk16_c*)  # configs 3 / 5 at the bench's 16 frames per step, small chunk sizes
+      w=${s#chunk16_}
+      for c in ${CHUNKS:-1 2 3 4}; do
+        run "bench16_${w}_chunk$c" 300 python bench.py --workload "$w" --steps 10 --warmup 3 --no-cpu-baseline --no-h2d --chunk "$c"
+      done ;;
     pmcsq2_c*) w=${s#pmcsq2_}; run "pmcsq2_$w" 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_ACTIVE_INST_ANY -d "$OUT/pmcsq2_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
     prof_c*) w=${s#prof_}; run "rocprof_stats_$w" 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 5 --warmup 2 --no-cpu-baseline --no-h2d ;;
     pmcsq_c*) w=${s#pmcsq_}; run "pmcsq_$w" 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/pmcsq_$w" -o run --output-format csv -- python3 bench.py --workload "$w" --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
