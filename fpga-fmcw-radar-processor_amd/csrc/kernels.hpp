@@ -1438,6 +1438,16 @@ __device__ __forceinline__ int xcd_block_id(int bid, int grid) {
 #define FMCW_K2_PF_NC 256  // measured: no gain at NC = 512, 1024 (profiles/r02/k2_pf); again after
                            // the one-site prefetch: NC 512 41.0 vs 41.2 us, NC 1024 62.8 vs 55.4 us
 #endif
+#ifndef FMCW_K2_PREFETCH_1024  // K2 at NC = 1024 (MTI off): none (8 or 16 points: slower, below)
+#define FMCW_K2_PREFETCH_1024 0
+#endif
+#ifndef FMCW_K2_PREFETCH_512  // K2 at NC = 512 (MTI off): points of the next unit loaded ahead
+#define FMCW_K2_PREFETCH_512 8  // half a unit: 165 instead of 178 VGPRs, so 3 waves per SIMD
+                                // instead of 2, and config-3 K2 41.6-41.9 -> 39.0-39.2 us per
+                                // launch (profiles/r03/k2/k2_pf_ab.log; 16 points: 42.1, 3 waves
+                                // without a prefetch: 42.2-42.5; at NC = 1024 both slower, 61-64
+                                // against 56 us)
+#endif
 #ifndef FMCW_K2_WAVES     // K2 waves per SIMD asked of the register allocator (0 = by geometry)
 #define FMCW_K2_WAVES 0
 #endif
@@ -1506,7 +1516,11 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
   // registers right after this unit's first pass has consumed its own, so a wave keeps 8 KiB
   // of HBM reads in flight through its FFT, magnitude, map store and CFAR phases instead of
   // exposing the full load latency once per unit.
-  constexpr int NPF = MTI == 0 && NC <= FMCW_K2_PF_NC ? FMCW_K2_PREFETCH : 0;  // points loaded ahead
+  constexpr int NPF = MTI != 0                ? 0
+                      : NC <= FMCW_K2_PF_NC     ? FMCW_K2_PREFETCH
+                      : NC == 512               ? FMCW_K2_PREFETCH_512
+                      : NC == 1024              ? FMCW_K2_PREFETCH_1024
+                                                : 0;  // points loaded ahead
   constexpr bool PF = NPF > 0;
   // Tile order.  FMCW_K2_ORDER 0: frame-minor over all waves (tile -> f = tile % nf).
   // Measured on config 2: order 1 cuts K2 0.905 -> 0.874 us/frame (map-store cost 0.13 -> 0.085).
