@@ -32,6 +32,9 @@ namespace fmcw {
 // config 3 neutral; config 5 (N = 8192) K1 64.9 -> 68.5 us per launch, so N <= 4096 only
 #define FMCW_K1_WT 1
 #endif
+#ifndef FMCW_K1_PX_POLICY   // k_range_px spectrum store cache policy bits (0 = write-back)
+#define FMCW_K1_PX_POLICY (FMCW_NT_SPEC_ST ? 2 : 0)
+#endif
 #ifndef FMCW_K2_BUFLD       // K2 prefetch through buffer loads with SGPR offsets (1) or global loads (0)
 #define FMCW_K2_BUFLD 1
 #endif
@@ -736,7 +739,7 @@ k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const floa
         typedef float f4v __attribute__((ext_vector_type(4)));
         const f4v x = {X[0][r].x, X[0][r].y, X[1][r].x, X[1][r].y};
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(fmcw_u4v, x), rs, vo, (4 * m + 64 * s) * ncb * 1024,
-                                               FMCW_NT_SPEC_ST ? 2 : 0);
+                                               FMCW_K1_PX_POLICY);
       }
   }
 }
