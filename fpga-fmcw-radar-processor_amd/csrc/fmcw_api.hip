@@ -673,6 +673,17 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
       (void)hipGetLastError();
     occupancy_grid(ci.fn, 256, h->cfar2d_smem, h->n_cu, &h->grid_cfar);
   }
+  // experiment knobs (tools/overlap_lab.py): cap a persistent grid so that another stream's
+  // kernels find free CU slots beside it
+  auto cap_grid = [](const char* name, int* g) {
+    if (const char* v = std::getenv(name)) {
+      const int n = std::atoi(v);
+      if (n > 0) *g = std::min(*g, n);
+    }
+  };
+  cap_grid("FMCW_GRID_RANGE", &h->grid_range);
+  cap_grid("FMCW_GRID_DOPPLER", &h->grid_doppler);
+  cap_grid("FMCW_GRID_CFAR", &h->grid_cfar);
   *out = h;
   return FMCW_OK;
 }
