@@ -184,7 +184,9 @@ typedef enum {
  * range-stage kernel the handle runs: 0 k_range (T chirps per workgroup), 1 k_range2 (two chirps
  * per thread), 2 k_range_sq (two chirps one after the other through one chirp's LDS; N = 4096,
  * 8192), 3 k_range_px (as 2 with two LDS exchanges and a cross-lane last pass; N = 8192);
- * environment FMCW_K1=single|dual|seq|px at fmcw_create caps the choice.
+ * environment FMCW_K1=single|dual|seq|px at fmcw_create caps the choice.  (Tuning experiments
+ * only: FMCW_CFAR2D_STEPS sets the 2-D CFAR strip length, FMCW_GRID_RANGE / _DOPPLER / _CFAR cap
+ * the persistent grids, each read at fmcw_create; results never depend on them.)
  * FMCW_INFO_WINDOW_SATURATIONS / FMCW_INFO_WORD_SATURATIONS: status words 2 / 3 of the last
  * fmcw_process call (fmcw_enqueue callers read them from n_dets_dev). */
 typedef enum { FMCW_INFO_CHUNK = 4, FMCW_INFO_RANGE_KERNEL = 6, FMCW_INFO_WINDOW_SATURATIONS = 7,
