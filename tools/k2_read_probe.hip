@@ -5,8 +5,9 @@
 //
 //   k2_rows8   K2's pattern: one range row per wave, lane t loads chirps t + 64 m (m < 16), 8 B
 //              each; the 4 waves of a workgroup take 4 consecutive rows; XCD-contiguous ids
-//   k2_rows16  the same rows, 16-B loads: lane t loads both chirps of tile (t & 31) + 32 m'
-//              (m' < 8) of row 2 * wave + (t >> 5)... i.e. 2 rows per wave, 8 loads per lane
+//   rows8_w*   k2_rows8 with 8 / 2 waves (rows) per workgroup, and without the XCD remap
+//   k2_rows16  16-B loads: lane t loads both chirps of tile (t & 31) + 32 m (m < 16) of row
+//              2 * wave + (t >> 5), i.e. 2 rows per wave, 16 loads per lane
 //   linear16   the same bytes front to back, 16 B per lane (the streaming ceiling)
 // usage: tools/k2_read_probe [frames=3] [reps=20]
 #include <hip/hip_runtime.h>
@@ -38,6 +39,25 @@ __global__ void __launch_bounds__(256) k2_rows8(const float2* __restrict__ s, in
     acc += v.x + v.y;
   }
   sink[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
+// as k2_rows8 with W waves per workgroup (W consecutive rows: W = 8 reads whole 128-B lines of
+// each tile) and the XCD-contiguous id remap on (X = 1) or off
+template <int W, int X>
+__global__ void __launch_bounds__(64 * W) k2_rows8w(const float2* __restrict__ s, int rows, float* __restrict__ sink) {
+  const int b = X ? xcd_id(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const int row = b * W + w;
+  if (row >= rows) return;
+  const int f = row / NS, r = row % NS;
+  const float2* p = s + (size_t)f * NS * NC;
+  float acc = 0.f;
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const float2 v = p[off_of(r, t + 64 * m)];
+    acc += v.x + v.y;
+  }
+  sink[blockIdx.x * 64 * W + threadIdx.x] = acc;
 }
 
 __global__ void __launch_bounds__(256) k2_rows16(const float4* __restrict__ s, int rows, float* __restrict__ sink) {
@@ -76,7 +96,7 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&s, bytes));
   CHECK(hipMemset(s, 0, bytes));
   const int g8 = rows / 4, g16 = rows / 8, glin = 256 * 8;
-  CHECK(hipMalloc(&sink, (size_t)(g8 > glin ? g8 : glin) * 256 * sizeof(float)));
+  CHECK(hipMalloc(&sink, (size_t)rows * 64 * sizeof(float) + (size_t)glin * 256 * sizeof(float)));
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
@@ -93,6 +113,10 @@ int main(int argc, char** argv) {
     printf("%-10s %8.1f us per pass over %zu MiB  = %6.0f GB/s\n", name, us, bytes >> 20, bytes / us * 1e-3);
   };
   run("k2_rows8", [&] { hipLaunchKernelGGL(k2_rows8, dim3(g8), dim3(256), 0, 0, s, rows, sink); });
+  run("rows8_w8", [&] { hipLaunchKernelGGL((k2_rows8w<8, 1>), dim3(rows / 8), dim3(512), 0, 0, s, rows, sink); });
+  run("rows8_w2", [&] { hipLaunchKernelGGL((k2_rows8w<2, 1>), dim3(rows / 2), dim3(128), 0, 0, s, rows, sink); });
+  run("rows8_nox", [&] { hipLaunchKernelGGL((k2_rows8w<4, 0>), dim3(rows / 4), dim3(256), 0, 0, s, rows, sink); });
+  run("rows8_w8nx", [&] { hipLaunchKernelGGL((k2_rows8w<8, 0>), dim3(rows / 8), dim3(512), 0, 0, s, rows, sink); });
   run("k2_rows16", [&] { hipLaunchKernelGGL(k2_rows16, dim3(g16), dim3(256), 0, 0, reinterpret_cast<const float4*>(s), rows, sink); });
   run("linear16", [&] { hipLaunchKernelGGL(linear16, dim3(glin), dim3(256), 0, 0, reinterpret_cast<const float4*>(s), bytes / 16, sink); });
   CHECK(hipGetLastError());
