@@ -8,6 +8,8 @@
 //   rows8_w*   k2_rows8 with 8 / 2 waves (rows) per workgroup, and without the XCD remap
 //   k2_rows16  16-B loads: lane t loads both chirps of tile (t & 31) + 32 m (m < 16) of row
 //              2 * wave + (t >> 5), i.e. 2 rows per wave, 16 loads per lane
+//   pairs32    2 rows per wave, lanes 2k / 2k + 1 load rows r / r + 1 of one tile: 32 contiguous
+//              bytes per tile and instruction (a K2 that would hold chirp pairs per lane)
 //   linear16   the same bytes front to back, 16 B per lane (the streaming ceiling)
 // usage: tools/k2_read_probe [frames=3] [reps=20]
 #include <hip/hip_runtime.h>
@@ -77,6 +79,25 @@ __global__ void __launch_bounds__(256) k2_rows16(const float4* __restrict__ s, i
   sink[blockIdx.x * 256 + threadIdx.x] = acc;
 }
 
+// two rows per wave with 32 contiguous bytes per tile and instruction: lanes 2k and 2k + 1 load
+// rows r and r + 1 (adjacent in the tile) of tile k + 32 m, both chirps (16 B) each
+__global__ void __launch_bounds__(256) k2_pairs32(const float4* __restrict__ s, int rows, float* __restrict__ sink) {
+  const int b = xcd_id(blockIdx.x, gridDim.x);
+  const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const int row = b * 8 + 2 * w + (t & 1);
+  if (row >= rows) return;
+  const int f = row / NS, r = row % NS;
+  const float2* p = reinterpret_cast<const float2*>(s) + (size_t)f * NS * NC;
+  float acc = 0.f;
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const int c = 2 * ((t >> 1) + 32 * m);
+    const float4 v = *reinterpret_cast<const float4*>(p + off_of(r, c));
+    acc += v.x + v.y + v.z + v.w;
+  }
+  sink[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
 __global__ void __launch_bounds__(256) linear16(const float4* __restrict__ s, size_t n4, float* __restrict__ sink) {
   float acc = 0.f;
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
@@ -118,6 +139,7 @@ int main(int argc, char** argv) {
   run("rows8_nox", [&] { hipLaunchKernelGGL((k2_rows8w<4, 0>), dim3(rows / 4), dim3(256), 0, 0, s, rows, sink); });
   run("rows8_w8nx", [&] { hipLaunchKernelGGL((k2_rows8w<8, 0>), dim3(rows / 8), dim3(512), 0, 0, s, rows, sink); });
   run("k2_rows16", [&] { hipLaunchKernelGGL(k2_rows16, dim3(g16), dim3(256), 0, 0, reinterpret_cast<const float4*>(s), rows, sink); });
+  run("pairs32", [&] { hipLaunchKernelGGL(k2_pairs32, dim3(g16), dim3(256), 0, 0, reinterpret_cast<const float4*>(s), rows, sink); });
   run("linear16", [&] { hipLaunchKernelGGL(linear16, dim3(glin), dim3(256), 0, 0, reinterpret_cast<const float4*>(s), bytes / 16, sink); });
   CHECK(hipGetLastError());
   CHECK(hipFree(s));
