@@ -12,14 +12,15 @@ namespace fmcw {
 // ---- K1: window + range FFT + corner turn -------------------------------------------------
 using RangeFn = void (*)(const void*, float2*, const float*, const float*, int, int, float, uint32_t*);
 // which range kernel family a handle runs (fmcw.h FMCW_INFO_RANGE_KERNEL)
-enum RangeKind { kRangeSingle = 0, kRangeDual = 1, kRangeSeq = 2, kRangePx = 3 };
+// (1 was round 2's dual kernel k_range2, removed in round 4; the id stays retired)
+enum RangeKind { kRangeSingle = 0, kRangeSeq = 2, kRangePx = 3 };
 struct RangeInfo {
   RangeFn fn;
   int T, RB, NT;   // chirps per group, range bins per 1 KiB tile, threads per workgroup
   int kind;        // RangeKind actually selected
 };
-// want = the preferred family (kRangePx: k_range_px at N = 8192; kRangeSeq: k_range_sq where
-// instantiated, else k_range2, else k_range); q15 / h16 select the RTL-compat window and the fp16 spectrum (k_range only)
+// want = the preferred family (kRangePx: k_range_px at N = 8192, kRangeSeq: k_range_sq at N = 4096,
+// else k_range); q15 / h16 select the RTL-compat window and the fp16 spectrum (k_range only)
 RangeInfo range_info(uint32_t n, int dtype, int window, bool h16, int want);
 
 // ---- K2: Doppler window + FFT + |X| / NCI + map + 1-D CFAR --------------------------------

@@ -378,51 +378,6 @@ __device__ __forceinline__ void stockham_from(float2* buf, int t) {
   }
 }
 
-// Stockham radix-16 passes on TWO transforms held in two buffers (the dual range kernel), from
-// sub-transform size L while more than 16 points remain after the pass: each thread's groups
-// get their twiddles once for both transforms.  Workgroup barriers (the transforms span waves).
-template <int N, int L, int P>
-__device__ __forceinline__ void dual_passes(float2* b0, float2* b1, int t) {
-  if constexpr (N / L > 16) {
-    constexpr int R = 16, G = N / R / P, S = N / R;
-    static_assert(G == 1, "one radix-16 group per thread and transform");
-    float2 v0[R], v1[R];
-    const int j = t;
-    {
-      const float2* s0 = b0 + pad16(j);
-      const float2* s1 = b1 + pad16(j);
-#pragma unroll
-      for (int m = 0; m < R; ++m) {
-        v0[m] = s0[padoff(m * S)];
-        v1[m] = s1[padoff(m * S)];
-      }
-    }
-    __syncthreads();
-    const int k = j & (L - 1);
-    if constexpr (L > 1) {
-      GroupTwiddles<R, L * R> tw;
-      tw.init(k);
-#pragma unroll
-      for (int m = 1; m < R; ++m) {
-        const float2 w = tw.pow(m);
-        v0[m] = cmul(v0[m], w);
-        v1[m] = cmul(v1[m], w);
-      }
-    }
-    Dft<R>::run(v0);
-    Dft<R>::run(v1);
-    float2* d0 = b0 + pad16((j / L) * L * R + k);
-    float2* d1 = b1 + pad16((j / L) * L * R + k);
-#pragma unroll
-    for (int m = 0; m < R; ++m) {
-      d0[padoff(m * L)] = v0[m];
-      d1[padoff(m * L)] = v1[m];
-    }
-    __syncthreads();
-    dual_passes<N, L * R, P>(b0, b1, t);
-  }
-}
-
 // Radix of the last pass when the passes start at sub-transform size L0.
 template <int N, int L0> struct FinalRadix {
   static constexpr int calc() {

@@ -168,7 +168,7 @@ struct fmcw_handle {
   int n_cu = 256;
   // range kernel geometry (runtime copies of RangeGeom<N>)
   int T = 0, RB = 0, lgT = 0, lgRB = 0;
-  int k1_want = kRangePx;   // preferred K1 family (environment FMCW_K1 at fmcw_create)
+  int k1_want = kRangePx;   // preferred K1 family (FMCW_LAB builds: environment FMCW_K1)
   int k1_kind = kRangeSingle;  // the family the handle runs
   bool k2_fast = false;    // K2 runs its FAST instantiation (fixed at fmcw_create)
   uint32_t chunk = 1;
@@ -199,7 +199,8 @@ struct fmcw_handle {
   int grid_range = 0, grid_doppler = 0, grid_cfar = 0;
   size_t cfar2d_smem = 0;
   size_t inter_bytes = 0;               // h->inter (chunk frames of the K1 -> K2 spectrum)
-  int cfar2_steps = 0;                  // 2-D CFAR steps per strip (0 = cost model; FMCW_CFAR2D_STEPS)
+  int cfar2_steps = 0;                  // 2-D CFAR steps per strip (0 = cost model; FMCW_PARAM_CFAR2D_STEPS)
+  int cfar2_steps_last = 0;             // the strip length of the last 2-D CFAR launch (FMCW_INFO_CFAR2D_STEPS)
   uint32_t last_status[2] = {0, 0};     // fmcw_process: status words 2, 3 of its last call
   // profiling
   bool profiling = false;
@@ -218,7 +219,11 @@ bool k2_fast(const fmcw_config& c) {
                        (c.cfar1d_ref == 8 && c.cfar1d_guard == 2 && (int)(2 * c.cfar1d_ref) - (int)c.cfar1d_rank <= 4 &&
                         !(c.compat_rtl & FMCW_COMPAT_CFAR));
   return c.mti_mode == FMCW_MTI_OFF && c.mag_mode != FMCW_MAG_AMBM && c.map_kind != FMCW_MAP_DB &&
-         c.window != FMCW_WIN_Q15_RTL && cfar_ok && !std::getenv("FMCW_K2_GENERIC");
+         c.window != FMCW_WIN_Q15_RTL && cfar_ok
+#if FMCW_LAB  // A/B builds only (tools/build_variants.sh): the generic kernel on a FAST configuration
+         && !std::getenv("FMCW_K2_GENERIC")
+#endif
+      ;
 }
 
 // 2-D CFAR derived parameters
@@ -309,6 +314,10 @@ int validate(const fmcw_config& c) {
     return fail(FMCW_EINVAL, "spectrum_dtype=%d unknown", c.spectrum_dtype);
   if (c.spectrum_dtype == FMCW_SPEC_F16 && (c.compat_rtl & FMCW_COMPAT_MTI))
     return fail(FMCW_EINVAL, "compat MTI is defined on the fp32 spectrum (spectrum_dtype F16)");
+  // the Q15 path rounds the corner-turned spectrum to int16 words (and windows them in K2): an fp16
+  // spectrum has 11 significant bits, so words above 2048 would already be quantised
+  if (c.spectrum_dtype == FMCW_SPEC_F16 && c.window == FMCW_WIN_Q15_RTL)
+    return fail(FMCW_EINVAL, "window Q15_RTL is defined on the fp32 spectrum (spectrum_dtype F16)");
   return FMCW_OK;
 }
 
@@ -439,6 +448,7 @@ int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipS
                                      : cfar2_steps_model(nf, tpf, h->grid_cfar, doppler_info(c.n_doppler).WR * 4, a.hr);
     const int n_strips = nf * ((tpf + steps - 1) / steps);
     const int grid = std::min(n_strips, h->grid_cfar);
+    h->cfar2_steps_last = steps;
     ProfScope ps(h, FMCW_K_CFAR2D, s);
     hipLaunchKernelGGL(ci.fn, dim3(grid), dim3(256), h->cfar2d_smem, s, map_chunk, (int)c.n_range,
                        n_strips, steps, frame0, tile0, a, sink);
@@ -594,11 +604,13 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   h->cfg = *cfg;
   const fmcw_config& c = h->cfg;
   h->n_cu = prop.multiProcessorCount;
-  // K1 family: k_range_px at N = 8192, the sequential-pair kernel at N = 4096, else the dual
-  // one (N >= 2048), else k_range; environment FMCW_K1=single|dual|seq|px caps it (A/B runs)
+  // K1 family: k_range_px at N = 8192, the sequential-pair kernel at N = 4096, else k_range.
+  // The release library reads no environment; FMCW_LAB builds (tools/build_variants.sh) take
+  // FMCW_K1=single|seq|px for A/B runs.
+#if FMCW_LAB
   if (const char* k1 = std::getenv("FMCW_K1"))
-    h->k1_want = !std::strcmp(k1, "single") ? kRangeSingle : !std::strcmp(k1, "dual") ? kRangeDual
-               : !std::strcmp(k1, "seq") ? kRangeSeq : kRangePx;
+    h->k1_want = !std::strcmp(k1, "single") ? kRangeSingle : !std::strcmp(k1, "seq") ? kRangeSeq : kRangePx;
+#endif
   h->k2_fast = k2_fast(c);
   const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, c.spectrum_dtype == FMCW_SPEC_F16, h->k1_want);
   h->k1_kind = ri.kind;
@@ -611,7 +623,9 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   occupancy_grid(ri.fn, ri.NT, 0, h->n_cu, &h->grid_range);
   const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype == FMCW_SPEC_F16, h->k2_fast);
   occupancy_grid(di.fn, di.NT, 0, h->n_cu, &h->grid_doppler);
+#if FMCW_LAB
   if (const char* cs = std::getenv("FMCW_CFAR2D_STEPS")) h->cfar2_steps = std::max(0, std::atoi(cs));
+#endif
   h->chunk = c.chunk_frames ? std::min<uint32_t>(c.chunk_frames, c.max_frames) : auto_chunk(h, frame_inter);
   auto cleanup = [&](int code) {
     fmcw_destroy(h);
@@ -673,6 +687,7 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
       (void)hipGetLastError();
     occupancy_grid(ci.fn, 256, h->cfar2d_smem, h->n_cu, &h->grid_cfar);
   }
+#if FMCW_LAB
   // experiment knobs (tools/overlap_lab.py): cap a persistent grid so that another stream's
   // kernels find free CU slots beside it
   auto cap_grid = [](const char* name, int* g) {
@@ -684,6 +699,7 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   cap_grid("FMCW_GRID_RANGE", &h->grid_range);
   cap_grid("FMCW_GRID_DOPPLER", &h->grid_doppler);
   cap_grid("FMCW_GRID_CFAR", &h->grid_cfar);
+#endif
   *out = h;
   return FMCW_OK;
 }
@@ -894,6 +910,17 @@ int fmcw_set_profiling(fmcw_handle* h, int enable) {
   return FMCW_OK;
 }
 
+int fmcw_set_param(fmcw_handle* h, int key, int64_t value) {
+  if (!h) return fail(FMCW_EINVAL, "null handle");
+  switch (key) {
+    case FMCW_PARAM_CFAR2D_STEPS:
+      if (value < 0 || value > (1 << 20)) return fail(FMCW_EINVAL, "cfar2d steps %lld (0 = cost model)", (long long)value);
+      h->cfar2_steps = (int)value;
+      return FMCW_OK;
+  }
+  return fail(FMCW_EINVAL, "fmcw_set_param: unknown key %d", key);
+}
+
 int fmcw_get_info(fmcw_handle* h, int key, int64_t* value) {
   if (!h || !value) return fail(FMCW_EINVAL, "null argument");
   switch (key) {
@@ -901,6 +928,7 @@ int fmcw_get_info(fmcw_handle* h, int key, int64_t* value) {
     case FMCW_INFO_RANGE_KERNEL: *value = h->k1_kind; return FMCW_OK;
     case FMCW_INFO_WINDOW_SATURATIONS: *value = h->last_status[0]; return FMCW_OK;
     case FMCW_INFO_WORD_SATURATIONS: *value = h->last_status[1]; return FMCW_OK;
+    case FMCW_INFO_CFAR2D_STEPS: *value = h->cfar2_steps_last; return FMCW_OK;
   }
   return fail(FMCW_EINVAL, "fmcw_get_info: unknown key %d", key);
 }

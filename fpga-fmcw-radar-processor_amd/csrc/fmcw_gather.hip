@@ -137,33 +137,51 @@ int fmcw_comm_create(const void* id, int n_ranks, int rank, int device_id, size_
     return gfail(FMCW_EHIP, "ncclCommInitRank: %s", ncclGetErrorString(r));
   }
   const size_t msg = (1 + wire_cap) * sizeof(fmcw_det);
+  // the check word of the collective below first: it is tiny, and a rank that cannot even get it
+  // aborts the communicator, so the other ranks' all-reduce fails instead of waiting for it
+  uint64_t* v = nullptr;
+  if (n_ranks > 1 && hipMalloc(reinterpret_cast<void**>(&v), 3 * sizeof(uint64_t)) != hipSuccess) {
+    (void)hipGetLastError();
+    ncclCommAbort(c->comm);
+    c->comm = nullptr;
+    fmcw_comm_destroy(c);
+    return gfail(FMCW_ENOMEM, "gather check word: hipMalloc failed (communicator aborted)");
+  }
+  // a failed buffer allocation is not returned at once: every rank still joins the all-reduce
+  // (with a failure flag), so a local failure fails the whole job instead of hanging the others
+  bool local_fail = false;
   if (hipMalloc(reinterpret_cast<void**>(&c->wire), msg) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&c->recv), msg * (size_t)n_ranks) != hipSuccess) {
     (void)hipGetLastError();
-    fmcw_comm_destroy(c);
-    return gfail(FMCW_ENOMEM, "gather buffers (%zu B per rank) failed", msg);
+    local_fail = true;
   }
   if (n_ranks > 1) {
-    // every rank must size its message alike (send / recv sizes match): one collective check here,
-    // the only host synchronisation of the communicator's life
-    uint64_t* v = nullptr;
-    uint64_t h[2] = {(uint64_t)wire_cap, ~(uint64_t)wire_cap};  // max of both = max and ~min
+    // every rank must size its message alike (send / recv sizes match) and have its buffers: one
+    // collective check here, the only host synchronisation of the communicator's life
+    uint64_t h[3] = {(uint64_t)wire_cap, ~(uint64_t)wire_cap, local_fail ? 1u : 0u};  // max: max, ~min, any failed
     ncclResult_t rr = ncclSuccess;
-    if (hipMalloc(reinterpret_cast<void**>(&v), sizeof h) != hipSuccess ||
-        hipMemcpy(v, h, sizeof h, hipMemcpyHostToDevice) != hipSuccess ||
-        (rr = ncclAllReduce(v, v, 2, ncclUint64, ncclMax, c->comm, nullptr)) != ncclSuccess ||
-        hipMemcpy(h, v, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) {
-      (void)hipGetLastError();
-      if (v) hipFree(v);
-      fmcw_comm_destroy(c);
-      return gfail(FMCW_EHIP, "wire_cap check (all-reduce): %s", ncclGetErrorString(rr));
-    }
+    const bool ok = hipMemcpy(v, h, sizeof h, hipMemcpyHostToDevice) == hipSuccess &&
+                    (rr = ncclAllReduce(v, v, 3, ncclUint64, ncclMax, c->comm, nullptr)) == ncclSuccess &&
+                    hipMemcpy(h, v, sizeof h, hipMemcpyDeviceToHost) == hipSuccess;
     hipFree(v);
+    if (!ok) {
+      (void)hipGetLastError();
+      fmcw_comm_destroy(c);
+      return gfail(FMCW_EHIP, "gather check (all-reduce): %s", ncclGetErrorString(rr));
+    }
+    if (h[2]) {
+      fmcw_comm_destroy(c);
+      return local_fail ? gfail(FMCW_ENOMEM, "gather buffers (%zu B per rank) failed", msg)
+                        : gfail(FMCW_ENOMEM, "gather buffers failed on another rank");
+    }
     if (h[0] != wire_cap || ~h[1] != wire_cap) {
       fmcw_comm_destroy(c);
       return gfail(FMCW_EINVAL, "wire_cap differs between ranks (this rank %zu, max %llu, min %llu)", wire_cap,
                    (unsigned long long)h[0], (unsigned long long)~h[1]);
     }
+  } else if (local_fail) {
+    fmcw_comm_destroy(c);
+    return gfail(FMCW_ENOMEM, "gather buffers (%zu B per rank) failed", msg);
   }
   *out = c;
   return FMCW_OK;

@@ -18,24 +18,10 @@ RangeFn range_fn(int dtype, bool q15, bool h16) {
   return h16 ? range_fn_t<N, true>(dtype, q15) : range_fn_t<N, false>(dtype, q15);
 }
 
-// k_range2 (dual): T = 2 geometries with several waves per transform (N >= 2048)
-template <int N>
-RangeFn range2_fn(int dtype) {
-  if constexpr (RangeGeom<N>::T == 2 && RangeGeom<N>::P >= 128) {
-    switch (dtype) {
-      case FMCW_IN_F32: return k_range2<N, LoadF32>;
-      case FMCW_IN_F16: return k_range2<N, LoadF16>;
-      case FMCW_IN_I16: return k_range2<N, LoadI16>;
-    }
-  }
-  return nullptr;
-}
-
-// k_range_sq (sequential pair, round 3): N = 4096 and 8192.  Per N the measured-fastest
-// (values per thread V, samples per load E, waves per SIMD W), tools/k1_lab.hip
+// k_range_sq (sequential pair, round 3): N = 4096, the measured-fastest values per thread V,
+// samples per load E and waves per SIMD W (tools/k1_lab.hip; at N = 8192 k_range_px is faster)
 template <int N> struct SqPick;
 template <> struct SqPick<4096> { static constexpr int V = 16, E = 1, W = 3; };
-template <> struct SqPick<8192> { static constexpr int V = 16, E = 2, W = 3; };
 template <int N>
 RangeInfo range_sq(int dtype) {
   using S = SqPick<N>;
@@ -64,22 +50,10 @@ RangeInfo range_px(int dtype) {
 
 RangeInfo range_info(uint32_t n, int dtype, int window, bool h16, int want) {
   const bool q15 = window == FMCW_WIN_Q15_RTL;
-  // the dual / sequential-pair kernels: fp32 window, fp32 spectrum
+  // the pair kernels: fp32 window, fp32 spectrum (the Q15 / fp16-spectrum paths run k_range)
   if (!q15 && !h16) {
     if (want >= kRangePx && FMCW_K1_PX && n == 8192) return range_px(dtype);
-    if (want >= kRangeSeq && FMCW_K1_SQ && n >= (uint32_t)FMCW_K1_SQ) {
-      switch (n) {
-        case 4096: return range_sq<4096>(dtype);
-        case 8192: return range_sq<8192>(dtype);
-      }
-    }
-    if (want >= kRangeDual && FMCW_K1_DUAL && n >= (uint32_t)FMCW_K1_DUAL) {
-      switch (n) {
-#define R2_(N) case N: if (RangeFn f = range2_fn<N>(dtype)) return {f, RangeGeom<N>::T, RangeGeom<N>::RB, RangeGeom<N>::P, kRangeDual}; break;
-        R2_(2048) R2_(4096) R2_(8192)
-#undef R2_
-      }
-    }
+    if (want >= kRangeSeq && FMCW_K1_SQ && n == 4096 && n >= (uint32_t)FMCW_K1_SQ) return range_sq<4096>(dtype);
   }
   switch (n) {
 #define R_(N) case N: return {range_fn<N>(dtype, q15, h16), RangeGeom<N>::T, RangeGeom<N>::RB, RangeGeom<N>::NT, kRangeSingle};

@@ -323,151 +323,31 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
       else st_f4<FMCW_NT_SPEC_ST>(dst + i * dstep, make_float4(v0.x, v0.y, v1.x, v1.y));
     }
   }
-  if constexpr (Q15) status_add(status, n_sat);  // status word 0: window saturations
+  if constexpr (Q15) status_add(status, n_sat);  // status word 2 (status = n_dets_dev + 2): window saturations
 }
 
 // --------------------------------------------------------------------------------------
-// K1 for T = 2 (N >= 2048), "dual": every thread carries the same 16 points of BOTH chirps of
-// the group (N / 16 threads instead of 2 N / 16), so the twiddles of a pass serve two
-// transforms, and the last pass ends in registers with X0[d] and X1[d] in the same lane -- the
-// 16-B (chirp 0, chirp 1) element of the tiled spectrum at range bin d -- so the tiles are
-// stored straight from registers: no transposing LDS read, one barrier pair fewer.  Lanes of a
-// wave hold consecutive d, so each store instruction writes whole 1 KiB tiles.
-// --------------------------------------------------------------------------------------
-#ifndef FMCW_K1_DUAL       // smallest N that runs the dual kernel (0: never)
-#define FMCW_K1_DUAL 4096
-#endif
-template <int N, typename LD>
-__global__ void __launch_bounds__(N / 16) __attribute__((amdgpu_waves_per_eu(1)))
-k_range2(const void* __restrict__ cube, float2* __restrict__ inter, const float* __restrict__ win,
-         const float* __restrict__ chirp_w, int nc, int n_groups, float /* q15_scale */, uint32_t* /* status */) {
-  using Gm = RangeGeom<N>;
-  constexpr int P = Gm::P, RB = Gm::RB, REG = Gm::REG;
-  static_assert(Gm::T == 2 && P >= 128, "two chirps per group, several waves per transform");
-  constexpr int T = 2;
-  __shared__ __attribute__((aligned(16))) float2 lds[T * REG];
-  float2* const buf0 = lds;
-  float2* const buf1 = lds + REG;
-  const int t0 = threadIdx.x;
-  const int ncb = nc / T;
-
-  typename LD::Raw a0[8], a1[8];
-  float cw0 = 1.f, cw1 = 1.f;
-  auto fetch = [&](int g) {
-    const int fr = g / ncb;
-    const int cb = g - fr * ncb;
-    const size_t chirp = (size_t)fr * nc + (size_t)cb * T;
-    const int t = opaque(t0);
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      a0[m] = LD::fetch(cube, chirp * N + 2 * t + (N / 8) * m);
-      a1[m] = LD::fetch(cube, (chirp + 1) * N + 2 * t + (N / 8) * m);
-    }
-    if (chirp_w) {
-      cw0 = chirp_w[__builtin_amdgcn_readfirstlane(cb * T)];
-      cw1 = chirp_w[__builtin_amdgcn_readfirstlane(cb * T + 1)];
-    }
-  };
-  float2 wh[8];  // range window, held
-#pragma unroll
-  for (int m = 0; m < 8; ++m) wh[m] = *reinterpret_cast<const float2*>(win + 2 * t0 + (N / 8) * m);
-#pragma unroll
-  for (int m = 0; m < 8; ++m) asm volatile("" ::"v"(wh[m].x), "v"(wh[m].y));
-  int g = blockIdx.x;
-  if (g < n_groups) fetch(g);
-
-  for (; g < n_groups; g += gridDim.x) {
-    const int fr = g / ncb;
-    const int cb = g - fr * ncb;
-    const int t = opaque(t0);
-    __syncthreads();  // the previous group's last-pass reads are done with lds
-    // pass 0: radix 8 from registers, both chirps
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      float4 ax[8];
-#pragma unroll
-      for (int m = 0; m < 8; ++m) ax[m] = LD::expand(q ? a1[m] : a0[m]);
-      const float cw = q ? cw1 : cw0;
-      float2* buf = q ? buf1 : buf0;
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        float2 v[8];
-#pragma unroll
-        for (int m = 0; m < 8; ++m) {
-          const float we = (e ? wh[m].y : wh[m].x) * cw;
-          v[m] = e ? make_float2(ax[m].z * we, ax[m].w * we) : make_float2(ax[m].x * we, ax[m].y * we);
-        }
-        Dft<8>::run(v);
-        float2* d = buf + pad16((2 * t + e) * 8);
-#pragma unroll
-        for (int m = 0; m < 8; ++m) d[m] = v[m];
-      }
-    }
-    if (g + (int)gridDim.x < n_groups) fetch(g + gridDim.x);
-    __syncthreads();
-    // LDS passes of radix 16 while more than 16 points remain after them, both chirps at once
-    dual_passes<N, 8, P>(buf0, buf1, t);
-    // last pass in registers, then the tile stores: lane t holds range bins d = j + m N / R
-    constexpr int L = N / FinalRadix<N, 8>::R;
-    constexpr int R = FinalRadix<N, 8>::R;
-    constexpr int G = N / R / P;
-#pragma unroll
-    for (int gg = 0; gg < G; ++gg) {
-      const int j = t + P * gg;
-      float2 x0[R], x1[R];
-      const float2* s0 = buf0 + pad16(j);
-      const float2* s1 = buf1 + pad16(j);
-#pragma unroll
-      for (int m = 0; m < R; ++m) {
-        x0[m] = s0[padoff(m * (N / R))];
-        x1[m] = s1[padoff(m * (N / R))];
-      }
-      GroupTwiddles<R, N> tw;
-      tw.init(j & (L - 1));
-#pragma unroll
-      for (int m = 1; m < R; ++m) {
-        const float2 w = tw.pow(m);
-        x0[m] = cmul(x0[m], w);
-        x1[m] = cmul(x1[m], w);
-      }
-      Dft<R>::run(x0);
-      Dft<R>::run(x1);
-      const size_t fbase = (size_t)fr * N * nc;
-#pragma unroll
-      for (int m = 0; m < R; ++m) {
-        const int d = j + m * (N / R);
-        const size_t off = fbase + ((size_t)(d / RB) * ncb + cb) * (RB * T) + (size_t)(d % RB) * T;
-        st_f4<FMCW_NT_SPEC_ST>(inter + off, make_float4(x0[m].x, x0[m].y, x1[m].x, x1[m].y));
-      }
-    }
-  }
-}
-
-// --------------------------------------------------------------------------------------
-// K1 "sequential pair" k_range_sq<N, LD, V, E> (N >= 2048, round 3).  Same input, window and
-// tiled output (T = 2: the 16-B (chirp 0, chirp 1) element per range bin) as k_range2, but the
-// two chirps of a group go through ONE chirp's worth of LDS one after the other: the first
-// chirp's spectrum waits in registers (V values per thread) while the second is transformed, then
-// both are stored as 16-B pairs straight from registers.  Half the LDS per workgroup doubles the
-// workgroups per CU (N = 8192: two of 68 KiB instead of one of 136 KiB; N = 4096: four), so one
-// workgroup's barriers and LDS passes overlap another's memory phases -- k_range2 at N = 8192 ran
-// one workgroup of 8 waves per CU and was latency-bound (round-2 verdict: 0.53 of HBM).
+// K1 "sequential pair" k_range_sq<N, LD, V, E> (the default at N = 4096, round 3).  T = 2 tiled
+// output (the 16-B (chirp 0, chirp 1) element per range bin), the two chirps of a group going
+// through ONE chirp's worth of LDS one after the other: the first chirp's spectrum waits in
+// registers (V values per thread) while the second is transformed, then both are stored as 16-B
+// pairs straight from registers.  Half the LDS of a two-chirp buffer doubles the workgroups per CU
+// (N = 4096: three of 34 KiB), so one workgroup's barriers and LDS passes overlap another's memory
+// phases.  (Round 2's "dual" kernel -- both chirps per thread in a two-chirp buffer, one workgroup
+// of 8 waves per CU at N = 8192 -- was latency-bound at 0.53 of HBM and is gone since round 4.)
 //   V = values per thread (16 or 32), P = N / V threads (one transform per workgroup pass);
 //   E = consecutive samples per lane per load: the first pass is a radix-(V/E) Stockham pass on
 //   the E groups j = E t + e, v[m] = x[j + m N/(V/E)] (E = 1: radix 16 from 8-B fp32 / 4-B fp16
 //   loads, so N = 4096 = 16^3 takes two LDS exchanges instead of three; E = 2: 16-B fp32 / 8-B fp16
-//   loads as k_range2).  Then radix-16 LDS passes while more than V points remain per group, and
-//   the last pass into registers: lane t holds X[j + m L] for j = t + P g, whole 1 KiB tiles per
-//   store instruction.
+//   loads).  Then radix-16 LDS passes while more than V points remain per group, and the last
+//   pass into registers: lane t holds X[j + m L] for j = t + P g, whole 1 KiB tiles per store
+//   instruction.
 // The next chirp's raw input is loaded as soon as this chirp's first pass has consumed its
 // registers (one chirp ahead, whatever group it belongs to), so the load overlaps three LDS passes.
 // Replaces the Xilinx range FFT (rtl/src/radar_core.vhd:303-316) + corner turner (:318-327).
 // --------------------------------------------------------------------------------------
-#ifndef FMCW_K1_SQ         // smallest N that runs k_range_sq (0: never)
+#ifndef FMCW_K1_SQ         // smallest N that runs k_range_sq (0: never; N = 8192 runs k_range_px)
 #define FMCW_K1_SQ 4096
-#endif
-#ifndef FMCW_K1_SQ_V8192   // values per thread of k_range_sq at N = 8192 (16 or 32)
-#define FMCW_K1_SQ_V8192 16
 #endif
 template <int N, int V> struct SqGeom {
   static constexpr int P = N / V;

@@ -29,7 +29,10 @@ COMM_ID_BYTES = 128
 K_RANGE, K_DOPPLER, K_CFAR2D, K_COMPACT, K_COUNT = 0, 1, 2, 3, 4
 KERNEL_NAMES = ("k_range", "k_doppler", "k_cfar", "k_compact")
 INFO_CHUNK, INFO_RANGE_KERNEL, INFO_WINDOW_SATURATIONS, INFO_WORD_SATURATIONS = 4, 6, 7, 8
-RANGE_KERNELS = ("k_range", "k_range2", "k_range_sq", "k_range_px")   # FMCW_INFO_RANGE_KERNEL 0..3
+INFO_CFAR2D_STEPS = 9
+PARAM_CFAR2D_STEPS = 1   # fmcw_set_param keys
+# FMCW_INFO_RANGE_KERNEL 0..3 (1 = round 2's k_range2, retired in ABI 6)
+RANGE_KERNELS = ("k_range", "k_range2 (retired)", "k_range_sq", "k_range_px")
 STATUS_WORDS = 4      # FMCW_STATUS_WORDS: n_dets_dev = found, lost, window / word saturations
 
 STATUS_NAMES = {0: "FMCW_OK", -1: "FMCW_EINVAL", -2: "FMCW_ENOMEM", -3: "FMCW_EHIP",
@@ -86,6 +89,7 @@ SIGNATURES = {
     "fmcw_cfar": (_I, [_VP, _VP, _SZ, _VP, _SZ, _VP, _VP]),
     "fmcw_set_profiling": (_I, [_VP, _I]),
     "fmcw_get_info": (_I, [_VP, _I, C.POINTER(C.c_int64)]),
+    "fmcw_set_param": (_I, [_VP, _I, C.c_int64]),
     "fmcw_kernel_times": (_I, [_VP, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "fmcw_reset_kernel_times": (_I, [_VP]),
     "fmcw_device_alloc": (_I, [_SZ, C.POINTER(_VP), _I]),

@@ -57,14 +57,18 @@ class RadarOutput:
     def det_doppler_bin(self):      # :35
         return self.dets["doppler"]
 
-    # status_overflow (radar_core.vhd:447-456) as counts: samples saturated by the RTL-compat
-    # integer windows, and int16 spectrum words / canceller outputs clipped (fmcw.h status words)
+    # status words 2 / 3 (fmcw.h): samples saturated by the RTL-compat integer windows, and int16
+    # spectrum words / canceller outputs clipped
     window_saturations: int = 0
     word_saturations: int = 0
 
     @property
     def status_overflow(self) -> bool:
-        return bool(self.window_saturations or self.word_saturations)
+        """The RTL's sticky flag (radar_core.vhd:447-456): set by the window multipliers'
+        saturation (win1_saturation / win2_saturation, :451) only.  The canceller's output
+        saturates silently in the RTL (doppler_notch.vhd:75-93), and this build's int16 word
+        clipping is counted separately in `word_saturations`, an extension outside the flag."""
+        return bool(self.window_saturations)
 
 
 def pack_adc_words(i: np.ndarray, q: np.ndarray) -> np.ndarray:
@@ -261,14 +265,21 @@ class RadarCore:
         L.check(self._lib.fmcw_kernel_times(self._h, ms, n))
         return {L.KERNEL_NAMES[k]: (ms[k], n[k]) for k in range(L.K_COUNT)}
 
+    def set_param(self, key: str, value: int) -> None:
+        """fmcw_set_param (tuning; results never depend on it): "cfar2d_steps" = 2-D CFAR steps
+        per strip, 0 = the library's cost model."""
+        k = {"cfar2d_steps": L.PARAM_CFAR2D_STEPS}[key]
+        L.check(self._lib.fmcw_set_param(self._h, k, int(value)))
+
     def info(self, key: str) -> int:
         """fmcw_get_info: "chunk" (frames per K1 -> K2 chunk), "range_kernel" (0 k_range,
-        1 k_range2, 2 k_range_sq), "window_saturations" / "word_saturations" (status words 2 / 3
-        of the last process() call: the sticky status_overflow of radar_core.vhd:447-456 as
-        counts)."""
+        2 k_range_sq, 3 k_range_px; 1 retired), "window_saturations" / "word_saturations" (status
+        words 2 / 3 of the last process() call; window_saturations is the sticky status_overflow
+        of radar_core.vhd:447-456 as a count), "cfar2d_steps" (strip length of the last 2-D CFAR
+        launch)."""
         k = {"chunk": L.INFO_CHUNK, "range_kernel": L.INFO_RANGE_KERNEL,
              "window_saturations": L.INFO_WINDOW_SATURATIONS,
-             "word_saturations": L.INFO_WORD_SATURATIONS}[key]
+             "word_saturations": L.INFO_WORD_SATURATIONS, "cfar2d_steps": L.INFO_CFAR2D_STEPS}[key]
         v = C.c_int64(0)
         L.check(self._lib.fmcw_get_info(self._h, k, C.byref(v)))
         return int(v.value)

@@ -56,14 +56,17 @@
 extern "C" {
 #endif
 
-#define FMCW_ABI_VERSION 5  /* 2: fmcw_config grew compat_rtl, range_shift (27 words, 108 B);
+#define FMCW_ABI_VERSION 6  /* 2: fmcw_config grew compat_rtl, range_shift (27 words, 108 B);
                                3: + spectrum_dtype (28 words, 112 B);
                                4: FMCW_K_COUNT 5 -> 6, FMCW_INFO_PAIR_CHUNK;
                                5: n_dets_dev holds FMCW_STATUS_WORDS (4) words (saturation
                                   counts); the fused / paired kernels are gone (FMCW_K_COUNT 4,
                                   info keys 1-3 and 5 retired, fmcw_get_fused_trace removed);
                                   FMCW_WIN_Q15_RTL also windows slow time in integers;
-                                  fmcw_comm_create takes wire_cap, fmcw_gather_dets det_cap */
+                                  fmcw_comm_create takes wire_cap, fmcw_gather_dets det_cap;
+                               6: fmcw_set_param (FMCW_PARAM_CFAR2D_STEPS), FMCW_INFO_CFAR2D_STEPS;
+                                  range-kernel id 1 (k_range2) retired; the library reads no
+                                  environment variable */
 
 typedef enum {
   FMCW_OK = 0,
@@ -181,16 +184,19 @@ typedef enum {
 } fmcw_kernel_id;
 
 /* fmcw_get_info keys.  FMCW_INFO_CHUNK: frames per K1 -> K2 chunk.  FMCW_INFO_RANGE_KERNEL: the
- * range-stage kernel the handle runs: 0 k_range (T chirps per workgroup), 1 k_range2 (two chirps
- * per thread), 2 k_range_sq (two chirps one after the other through one chirp's LDS; N = 4096,
- * 8192), 3 k_range_px (as 2 with two LDS exchanges and a cross-lane last pass; N = 8192);
- * environment FMCW_K1=single|dual|seq|px at fmcw_create caps the choice.  (Tuning experiments
- * only: FMCW_CFAR2D_STEPS sets the 2-D CFAR strip length, FMCW_GRID_RANGE / _DOPPLER / _CFAR cap
- * the persistent grids, each read at fmcw_create; results never depend on them.)
- * FMCW_INFO_WINDOW_SATURATIONS / FMCW_INFO_WORD_SATURATIONS: status words 2 / 3 of the last
- * fmcw_process call (fmcw_enqueue callers read them from n_dets_dev). */
+ * range-stage kernel the handle runs: 0 k_range (T chirps per workgroup; every N, and the Q15 /
+ * fp16-spectrum paths), 2 k_range_sq (two chirps one after the other through one chirp's LDS;
+ * N = 4096), 3 k_range_px (as 2 with two LDS exchanges and a cross-lane last pass; N = 8192);
+ * 1 (round 2's k_range2) is retired.  FMCW_INFO_WINDOW_SATURATIONS / FMCW_INFO_WORD_SATURATIONS:
+ * status words 2 / 3 of the last fmcw_process call (fmcw_enqueue callers read them from
+ * n_dets_dev).  FMCW_INFO_CFAR2D_STEPS: the strip length (workgroup steps) of the handle's last
+ * 2-D CFAR launch (0 before the first). */
 typedef enum { FMCW_INFO_CHUNK = 4, FMCW_INFO_RANGE_KERNEL = 6, FMCW_INFO_WINDOW_SATURATIONS = 7,
-               FMCW_INFO_WORD_SATURATIONS = 8 } fmcw_info_key;
+               FMCW_INFO_WORD_SATURATIONS = 8, FMCW_INFO_CFAR2D_STEPS = 9 } fmcw_info_key;
+
+/* fmcw_set_param keys (tuning; results never depend on them).  FMCW_PARAM_CFAR2D_STEPS: steps
+ * (4-wave-tile workgroup tiles) per 2-D CFAR strip, 0 = the library's cost model (default). */
+typedef enum { FMCW_PARAM_CFAR2D_STEPS = 1 } fmcw_param_key;
 
 /* Status words of fmcw_enqueue / fmcw_cfar (n_dets_dev). */
 #define FMCW_STATUS_WORDS 4
@@ -275,6 +281,7 @@ int fmcw_gather_compact_for_test(const fmcw_det* msgs_dev, int n_ranks, size_t w
  * its stream; fmcw_kernel_times synchronises and returns, per fmcw_kernel_id, the summed
  * milliseconds and the number of launches since the last reset. */
 int fmcw_set_profiling(fmcw_handle* h, int enable);
+int fmcw_set_param(fmcw_handle* h, int key, int64_t value);
 int fmcw_get_info(fmcw_handle* h, int key, int64_t* value);
 int fmcw_kernel_times(fmcw_handle* h, double* ms, uint64_t* launches);
 int fmcw_reset_kernel_times(fmcw_handle* h);

@@ -414,16 +414,18 @@ def test_repeated_launches_and_device_pointers(chunk):
 
 
 @pytest.mark.parametrize("steps", ["1", "3", "7", "0"])
-def test_cfar2d_strips_and_batched_launches(monkeypatch, steps):
+def test_cfar2d_strips_and_batched_launches(steps):
     """The 2-D CFAR walks strips of `steps` workgroup tiles through a ring of staged rows
     (cfar2d.hpp RowRing; 3 and 7 leave a short last strip per frame) and, on the caller's map,
     runs once per >= 16 frames (20 frames in chunks of 4: launches of 16 + 4).  Detections
     bit-exact vs the C oracle on the map the path wrote."""
-    monkeypatch.setenv("FMCW_CFAR2D_STEPS", steps)
     ns, nc, nf = 512, 128, 20
     cube = synth.frames(nf, ns, nc, 1, "two_targets")
     with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os2d", max_frames=nf, chunk_frames=4) as core:
+        core.set_param("cfar2d_steps", int(steps))
         out = core.process(cube)
+        if steps != "0":
+            assert core.info("cfar2d_steps") == int(steps)
     want = CB.cfar(out.rd_map, O.Cfar2D(), threads=16)
     np.testing.assert_array_equal(out.dets, want)
     assert out.n_dets > nf
@@ -475,11 +477,10 @@ def test_fp16_spectrum_ambm_and_stage_api():
     (2, 1, 3, 1, 50, (1, 3, 5), "3"),    # other window: runtime-geometry phase A
     (3, 0, 5, 3, 75, (2, 2, 2), "1"),    # no range guard, equal scales
 ])
-def test_cfar2d_geometries_and_ranks(monkeypatch, ref_r, guard_r, ref_d, guard_d, pct, scales, steps):
+def test_cfar2d_geometries_and_ranks(ref_r, guard_r, ref_d, guard_d, pct, scales, steps):
     """2-D CFAR at several windows, ranks and scale sets (oracle naming: ref/guard along range
     and Doppler), Rayleigh clutter with targets and a quiet patch, 3 frames; bit-exact vs the
     C oracle.  The pivoting k-th select runs at ranks other than 96 here."""
-    monkeypatch.setenv("FMCW_CFAR2D_STEPS", steps)
     rng = np.random.default_rng(ref_r * 100 + pct)
     m = rng.rayleigh(10.0, (3, 256, 128)).astype(np.float32)
     m[:, 100:120, 20:40] = rng.rayleigh(150.0, (3, 20, 20))
@@ -492,6 +493,7 @@ def test_cfar2d_geometries_and_ranks(monkeypatch, ref_r, guard_r, ref_d, guard_d
     with RadarCore(N_RANGE=256, N_DOPPLER=128, CFAR_REF_R=ref_d, CFAR_GUARD_R=guard_d, CFAR_REF_D=ref_r,
                    CFAR_GUARD_D=guard_r, cfar_rank_pct=pct, cfar_scales=scales, cfar="os2d",
                    max_frames=3) as core:
+        core.set_param("cfar2d_steps", int(steps))
         got, n, dropped = _stage_dets(core, m)
     assert dropped == 0
     want = CB.cfar(m, p, threads=16)

@@ -1,7 +1,8 @@
 """Round-3 GPU tests (libfmcw.so on gfx950 vs the CPU oracle, through the C-ABI):
 
-  * the three range-stage kernel families (k_range, k_range2, k_range_sq; fmcw.h
-    FMCW_INFO_RANGE_KERNEL) agree with each other and with the oracle at N = 2048..8192;
+  * the range-stage kernel family that ships for each N (k_range, k_range_sq at 4096, k_range_px
+    at 8192; fmcw.h FMCW_INFO_RANGE_KERNEL) is the one selected, and is on parity with the oracle
+    at N = 2048..8192;
   * the status words of the RTL-compat paths (fmcw.h n_dets_dev[2], [3]; the reference's sticky
     status_overflow, rtl/src/radar_core.vhd:447-456) count exactly what the integer oracle
     predicts, and stay 0 on the fp32 path;
@@ -19,61 +20,38 @@ from test_gpu_parity import check_map, oracle_dets, run_range_ct, to_complex
 
 pytestmark = pytest.mark.gpu
 
-KINDS = {"single": 0, "dual": 1, "seq": 2, "px": 3}
+KINDS = {"single": 0, "seq": 2, "px": 3}   # FMCW_INFO_RANGE_KERNEL (1 = k_range2, retired)
 
 
-def _run(monkeypatch, kind, **kw):
-    monkeypatch.setenv("FMCW_K1", kind)
-    cube = kw.pop("cube")
-    with RadarCore(**kw) as core:
-        got_kind = core.info("range_kernel")
-        out = core.process(cube)
-    return got_kind, out
-
-
-@pytest.mark.parametrize("ns,nc,nrx,dtype,mti", [
-    (8192, 32, 1, "f16", 0),     # config 5's range length (k_range_sq V16/E2 = k_range2's passes)
-    (8192, 64, 1, "i16", 2),     # MTI on: the Doppler window is applied by K2, not folded into K1
-    (4096, 64, 2, "f32", 0),     # config 3's range length: radix-16 first pass from 8-B loads
-    (4096, 32, 1, "i16", 3),
-    (2048, 64, 1, "f32", 0),     # below both: every family request falls back to k_range
+@pytest.mark.parametrize("ns,nc,nrx,dtype,mti,kind", [
+    (8192, 32, 1, "f16", 0, "px"),      # config 5's range length
+    (8192, 64, 1, "i16", 2, "px"),      # MTI on: the Doppler window is applied by K2, not folded into K1
+    (8192, 32, 1, "i16", 0, "px"),
+    (4096, 64, 2, "f32", 0, "seq"),     # config 3's range length: radix-16 first pass from 8-B loads
+    (4096, 32, 1, "i16", 3, "seq"),
+    (2048, 64, 1, "f32", 0, "single"),  # below both: k_range
 ])
-def test_range_kernel_families_agree(monkeypatch, ns, nc, nrx, dtype, mti):
-    """FMCW_K1=single|dual|seq|px: each family's map is on parity with the oracle (1e-4); where the
-    sequential-pair kernel runs the dual kernel's passes (N = 8192) they are bit-identical, the
-    permlane kernel (N = 8192) agrees with them to 1e-5, and the detections match the oracle CFAR
-    on each map bit for bit."""
+def test_shipped_range_kernel_families(ns, nc, nrx, dtype, mti, kind):
+    """The release library selects exactly one K1 family per N (no environment knob since ABI 6)
+    and its map is on parity with the oracle (1e-4), detections bit-exact vs the oracle CFAR on
+    the GPU's map.  (k_range at N = 4096 / 8192 ships for the Q15 and fp16-spectrum paths and is
+    tested there: test_range_ct_q15_rtl, test_fp16_spectrum.)"""
     nf = 2
     cube = synth.frames(nf, ns, nc, nrx, "two_targets", dtype=dtype, seed=17)
-    outs = {}
-    for kind in ("single", "dual", "seq", "px"):
-        got, out = _run(monkeypatch, kind, cube=cube, N_RANGE=ns, N_DOPPLER=nc, N_RX=nrx, in_dtype=dtype,
-                        cfar="os1d", max_frames=nf, mti_bypass=mti == 0, NOTCH_MODE=mti or 2)
-        # k_range2 from N = 4096 (FMCW_K1_DUAL), k_range_sq at 4096 / 8192, k_range_px at 8192
-        # (px asked at 4096 gives k_range_sq): below, k_range
-        want = KINDS[kind] if ns >= 4096 else KINDS["single"]
-        if kind == "px" and ns != 8192:
-            want = KINDS["seq"] if ns >= 4096 else KINDS["single"]
-        assert got == want, (kind, got)
-        outs[kind] = out
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, N_RX=nrx, in_dtype=dtype, cfar="os1d", max_frames=nf,
+                   mti_bypass=mti == 0, NOTCH_MODE=mti or 2) as core:
+        assert core.info("range_kernel") == KINDS[kind]
+        out = core.process(cube)
     ref = np.stack([O.process(to_complex(cube[f], dtype), None, mti_mode=mti)["mag"] for f in range(nf)])
-    for kind, out in outs.items():
-        check_map(out.rd_map, ref)
-        np.testing.assert_array_equal(out.dets, oracle_dets(out.rd_map, O.Cfar1D()))
-    np.testing.assert_array_equal(outs["single"].rd_map, outs["dual"].rd_map)
-    if ns == 8192:
-        np.testing.assert_array_equal(outs["seq"].rd_map, outs["dual"].rd_map)
-        assert rel_err(outs["px"].rd_map, outs["dual"].rd_map) <= 1e-5
-    else:
-        assert rel_err(outs["seq"].rd_map, outs["dual"].rd_map) <= 1e-5
+    check_map(out.rd_map, ref)
+    np.testing.assert_array_equal(out.dets, oracle_dets(out.rd_map, O.Cfar1D()))
 
 
 @pytest.mark.parametrize("dtype", ["f16", "f32", "i16"])
-def test_range_ct_px_many_groups(monkeypatch, dtype):
+def test_range_ct_px_many_groups(dtype):
     """k_range_px (N = 8192) over many chirp groups per workgroup and an odd group count per
     launch, every input word type: the canonical corner-turned spectrum vs the oracle, both chirps
     of every group (the permlane last pass and the half-wave tile stores)."""
-    monkeypatch.setenv("FMCW_K1", "px")
     ns, nc, nf = 8192, 128, 11     # 704 chirp pairs: more than one per resident workgroup
     cube = synth.frames(nf, ns, nc, 1, "random_target", dtype=dtype, seed=29)
     with RadarCore(N_RANGE=ns, N_DOPPLER=nc, in_dtype=dtype, cfar="none", max_frames=nf) as core:
@@ -88,11 +66,10 @@ def test_range_ct_px_many_groups(monkeypatch, dtype):
         assert rel_err(got[f], ref) <= 1e-4, f
 
 
-def test_range_ct_seq_many_groups(monkeypatch):
+def test_range_ct_seq_many_groups():
     """k_range_sq over many chirp groups per workgroup (the grid-stride loop with the one-chirp
     lookahead crossing group boundaries), an odd number of groups per launch: the canonical
     corner-turned spectrum vs the oracle, both chirps of every group."""
-    monkeypatch.setenv("FMCW_K1", "seq")
     ns, nc, nf = 4096, 128, 5
     cube = synth.frames(nf, ns, nc, 1, "random_target", dtype="f32", seed=23)
     with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="none", max_frames=nf) as core:

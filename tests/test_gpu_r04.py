@@ -1,0 +1,49 @@
+"""Round-4 GPU tests (libfmcw.so on gfx950 vs the CPU oracle, through the C-ABI).
+
+  * BASELINE configs 3 and 5 at the bench's OWN shape (bench.py WORKLOADS): 16 frames per call,
+    the library's auto chunk (3 frames per K1 -> K2 launch pair) and one 2-D CFAR launch over all
+    16 frames with the cost model's strip length -- exactly the composition whose time the driver
+    credits.  Maps of the first and last frame within 1e-4 of the fp64 oracle (the fp16-dequantised
+    input at config 5), every frame's detections bit-exact against the C oracle's 2-D OS-CFAR on
+    the GPU's map (oracle/fmcw_cpu.c, pinned to the NumPy oracle by tests/test_cpu_backend.py).
+    Semantics: rtl/src/radar_core.vhd:303-390, rtl/src/os_cfar_2d.vhd:152-217.
+"""
+import sys
+
+import numpy as np
+import pytest
+
+import cpu_backend as CB
+import fmcw_oracle as O
+from conftest import REPO
+from fmcw import RadarCore, synth
+from test_gpu_parity import check_map, to_complex
+
+pytestmark = pytest.mark.gpu
+
+if str(REPO) not in sys.path:
+    sys.path.insert(0, str(REPO))
+
+
+@pytest.mark.parametrize("wl", ["c3", "c5"])
+def test_bench_shape_parity(wl):
+    import bench  # the workload table the bench times (imports nothing heavy at module level)
+    w = bench.WORKLOADS[wl]
+    F, ns, nc, nrx, dtype = w["frames"], w["ns"], w["nc"], w["nrx"], w["dtype"]
+    assert F == 16
+    # bench.run_workload at rank 0: 16 distinct frames, seed 1234 + first global frame
+    cube = synth.frames(F, ns, nc, nrx, w["recipe"], seed=1234, dtype=dtype)
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, N_RX=nrx, in_dtype=dtype, cfar=w["cfar"], max_frames=F) as core:
+        assert core.info("chunk") == 3
+        out = core.process(cube)
+        steps = core.info("cfar2d_steps")
+    # the cost model's strip length for 16 frames (config 5: 32 steps of 16 rows; config 3 ~11)
+    assert steps >= 8, steps
+    for f in (0, F - 1):
+        ref = O.process(to_complex(cube[f], dtype), None)["mag"]
+        check_map(out.rd_map[f:f + 1], ref[None])
+    want = CB.cfar(out.rd_map, O.Cfar2D(), threads=16)
+    np.testing.assert_array_equal(out.dets, want)
+    assert set(out.dets["frame"].tolist()) == set(range(F))
+    hit = set(zip(out.dets["frame"].tolist(), out.dets["range"].tolist(), out.dets["doppler"].tolist()))
+    assert (0, round(100 * ns / 1024), 5) in hit and (F - 1, round(100 * ns / 1024), 5) in hit

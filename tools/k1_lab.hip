@@ -3,7 +3,8 @@
 // Run:   tools/k1_lab <N> <n_chirps> <n_rx> <frames> <f16:0|1> [reps]
 // Fills a deterministic cube on the device, runs every K1 variant instantiated for N over the
 // same frames, reports each one's average launch time (HIP events), its algorithmic HBM rate
-// (cube in + fp32 tiled spectrum out), and its max |diff| / max |ref| against k_range2.
+// (cube in + fp32 tiled spectrum out), and its max |diff| / max |ref| against k_range (the first
+// variant; round 2's dual kernel k_range2, the former reference, left the library in round 4).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -66,7 +67,6 @@ struct Var {
 
 template <int N, typename LD>
 void add_vars(std::vector<Var>& v) {
-  v.push_back({"k_range2", k_range2<N, LD>, N / 16});
   v.push_back({"k_range", k_range<N, LD>, RangeGeom<N>::NT});
   v.push_back({"sq_v16_e1", k_range_sq<N, LD, 16, 1>, N / 16});
   v.push_back({"sq_v16_e2", k_range_sq<N, LD, 16, 2>, N / 16});
