@@ -122,58 +122,126 @@ constexpr size_t cfar2d_smem_bytes(int hr) {
   return (size_t)(G::TR + 2 * hr) * (G::RB + 2 * G::KRS) + kCfar2dList * 4;
 }
 
-// Screen (compile-time HD <= 8 / GD) over disjoint PAIRS of Doppler-adjacent references: a pair
-// whose max key is >= cut_key7 holds at least one reference with fl(s_min * ref) >= cut, so
-// #{such pairs} is a lower bound on E(s_min) = #{fl(s_min * ref) >= cut}, and a cell whose bound
-// reaches need = n_ref - k cannot detect at any admissible scale.  (The max bound beats 2 x
-// #{pairs whose min qualifies} where it matters: for a reference exceeding the cut's level with
-// probability p it rejects from p ~ 0.32 instead of p ~ 0.52.)  A reference row of 2 HD + 1
-// cells gives HD pairs (its last cell is left out), a guard row two segments of HD - GD cells,
-// (HD - GD) / 2 pairs each.  Four CUTs per dword: Y[p] holds the cut keys of CUTs 4p..4p+3 in
-// its bytes, X the four pair-max bytes (bit 7 set) at the same offset from each, and bit 7 of
-// each byte of X - Y is set iff that pair counts (no byte borrows: X >= 128 > Y - 1); the
-// per-CUT counts (<= 60 < 256) accumulate in the bytes of acc[p] as (t >> 7) & 0x01010101.
-// Per window row: two 16-B LDS reads, <= 6 v_alignbyte for the unaligned X, and 4 VALU per 4
-// (CUT, pair) tests.
-template <int NC, int HD, int GD>
-__device__ __forceinline__ uint32_t cfar2d_screen7(const RowRing& rr, int rl, int d0, const Cfar2DArgs& a,
-                                                   int need, const uint32_t (&Y)[4]) {
-  static_assert(HD >= 1 && HD <= 8, "the window is inside the two 16-B reads");
-  constexpr int SEG = HD - GD, NPS = SEG / 2;
-  constexpr int B0 = 8 - HD;  // byte of cell d0 - HD in the window
-  uint32_t acc[4] = {0u, 0u, 0u, 0u};
-  for (int dr = -a.hr; dr <= a.hr; ++dr) {
-    const uint8_t* rp = rr.row(rl + a.hr + dr) + b7idx(d0 - 8);
-    uint32_t D[8];  // D[j] = pair-max bytes of cells d0 - 8 + 4j .. + 3
-    {
-      const uint4 q0 = *reinterpret_cast<const uint4*>(rp), q1 = *reinterpret_cast<const uint4*>(rp + 16);
-      D[0] = q0.x; D[1] = q0.y; D[2] = q0.z; D[3] = q0.w;
-      D[4] = q1.x; D[5] = q1.y; D[6] = q1.z; D[7] = q1.w;
-    }
-    auto X = [&](int b) -> uint32_t {  // bytes b .. b + 3 of the window (b compile-time after unrolling)
-      return (b & 3) ? __builtin_amdgcn_alignbyte(D[(b >> 2) + 1], D[b >> 2], (uint32_t)(b & 3)) : D[b >> 2];
-    };
-    auto count = [&](int p, uint32_t x) { acc[p] += ((x - Y[p]) >> 7) & 0x01010101u; };
-    if (dr >= -a.gr && dr <= a.gr) {  // guard row (uniform branch)
+// ---- Level screen (round 4; the reference window: HD 6, GD 2, HR <= 7, GR <= 1) ----------------
+// Exact reference counts at two fixed LEVELS per strip instead of a pair bound per CUT threshold.
+// For a level key Q, count_Q(c) = #{ref r of CUT c : key16(r) >= Q} is a box count: (2 HR + 1) x
+// 13 window minus the 3 x 5 guard block, separable into column sums over the staged rows and
+// sliding row sums of those.  Every ref counted lies >= lo(Q), so fl(s_min r) >= P = fl(s_min lo(Q))
+// (rounding is monotone); a CUT with key16(cut) < U = key16(P) has cut < lo(U) <= P.  So
+// key16(cut) < U and count_Q >= need give E(s_min) >= need: the cell cannot detect at any scale
+// >= s_min.  Two levels A <= B per strip, at the FMCW_K3_LV_QA / _QB quantiles (56 % / 68 %) of
+// the key7 levels of the strip's first 4096 cells: a CUT is screened out if either level rules it
+// out.  Quantiles, not offsets from the mean, so the levels follow the clutter's spread (config 3's
+// 4-rx NCI cells are far narrower than config 5's Rayleigh ones).  Survivors on the bench maps
+// (tests' fixed seed, NumPy model of this screen): config 5 1.6 %, config 2 1.7 %, config 3
+// 0.014 % -- the round-3 pair screen 1.9 %, 2.0 %, 0.010 % -- at about a quarter of its VALU work.
+// Ring rows hold per cell one byte: bit 0 = key >= QA, bit 4 = key >= QB, so both levels' column
+// sums (<= 2 HR + 1 <= 15) add in the nibbles of one 32-bit add; the 13-cell row sums (<= 143) of
+// each level are taken from byte prefix sums, the guard block's 5-cell sums (<= 15) in nibbles.
+#ifndef FMCW_K3_LV_QA  // the two levels: quantiles (per mille) of the strip's first-step cells
+#define FMCW_K3_LV_QA 560
+#endif
+#ifndef FMCW_K3_LV_QB
+#define FMCW_K3_LV_QB 680
+#endif
+// level nibbles of 4 cells from their key16 pairs (cells d, d + 1 | d + 2, d + 3): (k | 0x8000) - Q has
+// bit 15 set iff k >= Q (k < 0x8000, 1 <= Q <= 0x8000: no borrow across the halves); the byte
+// permute collects bits 15 / 31 of both words as bit 7 of 4 bytes
+__device__ __forceinline__ uint32_t lv_nibbles(uint2 kw, uint32_t qa2, uint32_t qb2) {
+  const uint32_t x0 = kw.x | 0x80008000u, x1 = kw.y | 0x80008000u;
+  const uint32_t pa = __builtin_amdgcn_perm(x1 - qa2, x0 - qa2, 0x07050301u);
+  const uint32_t pb = __builtin_amdgcn_perm(x1 - qb2, x0 - qb2, 0x07050301u);
+  return ((pa >> 7) & 0x01010101u) | ((pb >> 3) & 0x10101010u);
+}
+// byte-wise inclusive prefix sums of a word (bytes <= 63: no carry)
+__device__ __forceinline__ uint32_t byte_prefix(uint32_t x) {
+  x += x << 8;
+  return x + (x << 16);
+}
+// 13-cell sums of one level's column counts: b[i] = cell d0 - 6 + i in X[0..6]; out m (0..3) byte t
+// = sum b[4m + t .. 4m + t + 12] = (T_m - PE_m[t]) + T_{m+1} + T_{m+2} + PF_{m+3}[t] with T = word sums,
+// PF / PE the inclusive / exclusive byte prefixes (PE = PF - X); every byte stays in 0..143
+__device__ __forceinline__ void lv_sum13(const uint32_t (&X)[7], uint32_t (&H)[4]) {
+  uint32_t PF[7];
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
+  for (int k = 0; k < 7; ++k) PF[k] = byte_prefix(X[k]);
 #pragma unroll
-        for (int j = 0; j < NPS; ++j) {
-          count(p, X(B0 + 4 * p + 2 * j));
-          count(p, X(B0 + 4 * p + HD + GD + 1 + 2 * j));
-        }
-    } else {
-#pragma unroll
-      for (int p = 0; p < 4; ++p)
-#pragma unroll
-        for (int j = 0; j < HD; ++j) count(p, X(B0 + 4 * p + 2 * j));
-    }
+  for (int m = 0; m < 4; ++m) {
+    const uint32_t t3 = PF[m] + PF[m + 1] + PF[m + 2];           // byte 3 = T_m + T_{m+1} + T_{m+2} (<= 132)
+    const uint32_t tb = __builtin_amdgcn_perm(t3, t3, 0x03030303u);  // broadcast
+    H[m] = tb - PF[m] + X[m] + PF[m + 3];
   }
+}
+// Survivor bits (bit j = cell d0 + j may detect) of this lane's 16 CUTs, CUT row rl of the group
+// tile.  wa2 / wb2 = per level (U | 0x80008000) - 0x00010001 in both halves: W - key16 has bit 15
+// set iff key16 < U.
+template <int NC, int HR, int GR>
+__device__ __forceinline__ uint32_t cfar2d_screen_lv(const RowRing& rr, int rl, int d0, int need, uint32_t wa2,
+                                                     uint32_t wb2) {
+  static_assert(2 * HR + 1 <= 15 && 5 * (2 * GR + 1) <= 15, "nibble column sums and guard-row sums");
+  // column sums of the nibble rows: V over the 2 HR + 1 window rows (cells d0 - 8 .. d0 + 23), G over
+  // the 2 GR + 1 guard rows (cells d0 - 4 .. d0 + 19 = V words 1..6)
+  uint32_t V[8], G[6];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) V[k] = 0u;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) G[k] = 0u;
+  int sl = rr.slot(rl);  // ring slot of window row dr = -HR, advanced with wrap
+#pragma unroll
+  for (int dr = -HR; dr <= HR; ++dr) {
+    const uint8_t* rp = rr.tile + sl * rr.rs + b7idx(d0 - 8);
+    const uint4 q0 = *reinterpret_cast<const uint4*>(rp), q1 = *reinterpret_cast<const uint4*>(rp + 16);
+    const uint32_t D[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) V[k] += D[k];
+    if (dr >= -GR && dr <= GR) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) G[k] += D[k + 1];
+    }
+    sl = sl + 1 == rr.nr ? 0 : sl + 1;
+  }
+  // 13-cell window per level: realign so that word k byte t = cell d0 - 6 + 4k + t, then unpack
+  uint32_t HA[4], HB[4];
+  {
+    uint32_t XA[7], XB[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const uint32_t w = __builtin_amdgcn_alignbyte(V[k + 1], V[k], 2);
+      XA[k] = w & 0x0F0F0F0Fu;
+      XB[k] = (w >> 4) & 0x0F0F0F0Fu;
+    }
+    lv_sum13(XA, HA);
+    lv_sum13(XB, HB);
+  }
+  // guard block (3 x 5 around the CUT) per level, both levels in the nibbles (sums <= 15):
+  // g[i] = cell d0 - 2 + i; out m byte t = g[4m + t .. 4m + t + 4]
+  uint32_t H5[4];
+  {
+    uint32_t Gp[5], S2[5], S4[4];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) Gp[k] = __builtin_amdgcn_alignbyte(G[k + 1], G[k], 2);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) S2[k] = Gp[k] + __builtin_amdgcn_alignbyte(k < 4 ? Gp[k + 1] : 0u, Gp[k], 1);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) S4[k] = S2[k] + __builtin_amdgcn_alignbyte(S2[k + 1], S2[k], 2);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) H5[m] = S4[m] + Gp[m + 1];
+  }
+  // the CUTs' key16 (the staged row): W - key16 bit 15 = key16(cut) < U, gathered as byte bit 7
+  const uint16_t* kr = rr.krow(rl + HR) + k16idx(d0);
+  const uint4 ka = *reinterpret_cast<const uint4*>(kr), kc = *reinterpret_cast<const uint4*>(kr + 8);
+  const uint32_t kw[8] = {ka.x, ka.y, ka.z, ka.w, kc.x, kc.y, kc.z, kc.w};
+  const uint32_t add_need = (uint32_t)(128 - need) * 0x01010101u;  // count >= need <=> bit 7 of count + 128 - need
   uint32_t bits = 0;
 #pragma unroll
-  for (int p = 0; p < 4; ++p)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) bits |= (((acc[p] >> (8 * q)) & 0xffu) < (uint32_t)need ? 1u : 0u) << (4 * p + q);
+  for (int m = 0; m < 4; ++m) {
+    const uint32_t ca = __builtin_amdgcn_perm(wa2 - kw[2 * m + 1], wa2 - kw[2 * m], 0x07050301u);
+    const uint32_t cb = __builtin_amdgcn_perm(wb2 - kw[2 * m + 1], wb2 - kw[2 * m], 0x07050301u);
+    const uint32_t na = HA[m] - (H5[m] & 0x0F0F0F0Fu) + add_need;
+    const uint32_t nb = HB[m] - ((H5[m] >> 4) & 0x0F0F0F0Fu) + add_need;
+    const uint32_t surv = ~((na & ca) | (nb & cb)) & 0x80808080u;
+    bits |= ((surv * 0x00204081u) >> 28) << (4 * m);  // bit 7 of byte t -> bit 28 + t
+  }
   return bits;
 }
 
@@ -364,10 +432,14 @@ __device__ __forceinline__ uint32_t wave_select_kth(uint32_t ka, uint32_t kb, ui
 #define FMCW_K3_WAVES 3
 #endif
 
-template <int NC, int HD, int GD>
+// HD > 0: the reference window (HD 6, GD 2, compile-time HR / GR) with the level screen; HD == 0:
+// any window, runtime geometry, the pair screen on 7-bit keys (cfar2d_screen7_generic).
+template <int NC, int HD, int GD, int HR = 0, int GR = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FMCW_K3_WAVES)))
 k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int frame0, int tile0, Cfar2DArgs a,
          DetSink sink) {
+  constexpr bool LV = HD > 0;
+  static_assert(!LV || (HD == 6 && GD == 2 && HR >= 1), "the level screen is built for the reference window");
   using Gm = Cfar2DGeom<NC>;
   constexpr int WR = Gm::WR, NT = Gm::NT, RB = Gm::RB, TPR = Gm::TPR, WPB = Gm::WPB, TR = Gm::TR;
   static_assert(TR * NC == 4 * 4 * NT, "a step's new rows are 4 float4 per thread");
@@ -393,14 +465,24 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
   uint32_t* const cnt = aux + kCoopRound;
   const int tid = opaque(threadIdx.x);
 
-  // one float4 of cells (row x, Doppler d..d+3) plus the cell d+4 after it (circularly) into
-  // the ring as 4 pair-max key bytes, with its circular-halo copy
-  auto put4 = [&](const RowRing& rr, int x, int d, float4 v, float v4, int kb) {
+  // one float4 of cells (row x, Doppler d..d+3) into the ring, with its circular-halo copy: the
+  // key16 of each cell, and 4 bytes of the screen row -- LV: level nibbles; else the pair-max 7-bit
+  // keys (which need the cell d+4 after it, circularly, in v4)
+  // per strip: LV level words (qa2, qb2), else the 7-bit key base kb
+  uint32_t qa2 = 0u, qb2 = 0u;
+  int kb = 0;
+  auto put4 = [&](const RowRing& rr, int x, int d, float4 v, float v4) {
     v = a.compat ? q17x4(v) : nonneg4(v);
-    v4 = a.compat ? q17(v4) : nonneg(v4);
-    const uint32_t k0 = key7(v.x, kb), k1 = key7(v.y, kb), k2 = key7(v.z, kb), k3 = key7(v.w, kb), k4 = key7(v4, kb);
-    const uint32_t w = max(k0, k1) | (max(k1, k2) << 8) | (max(k2, k3) << 16) | (max(k3, k4) << 24) | 0x80808080u;
     const uint2 kw = make_uint2(key16(v.x) | (key16(v.y) << 16), key16(v.z) | (key16(v.w) << 16));
+    uint32_t w;
+    if constexpr (LV) {
+      (void)v4;
+      w = lv_nibbles(kw, qa2, qb2);
+    } else {
+      v4 = a.compat ? q17(v4) : nonneg(v4);
+      const uint32_t k0 = key7(v.x, kb), k1 = key7(v.y, kb), k2 = key7(v.z, kb), k3 = key7(v.w, kb), k4 = key7(v4, kb);
+      w = max(k0, k1) | (max(k1, k2) << 8) | (max(k2, k3) << 16) | (max(k3, k4) << 24) | 0x80808080u;
+    }
     uint8_t* row = rr.row(x);
     uint16_t* krow = rr.krow(x);
     *reinterpret_cast<uint32_t*>(row + b7idx(d)) = w;
@@ -429,9 +511,12 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
     RowRing rr{tile, keys, 0, nr, RB, Gm::KRS};
     float4 pre[4];
     float pre4[4];
-    // the strip's key base: mean level of the first step's CUT rows minus FMCW_K3_KEY_LOW
-    int kb;
+    // the strip's levels (LV) or key base, from the first step's CUT rows (TR x NC = 4096 cells):
+    // their mean level (bits >> 19: 16 levels per octave); LV then the FMCW_K3_LV_QA / _QB quantiles
+    // of a 128-level histogram around that mean
+    uint32_t wa2 = 0u, wb2 = 0u;
     {
+      uint32_t k7[16];
       uint32_t s = 0;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -440,19 +525,58 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
         const int rs = min(t_beg * TR + i, ns - 1);
         float4 v = *reinterpret_cast<const float4*>(fm + (size_t)rs * NC + d);
         v = a.compat ? q17x4(v) : nonneg4(v);
-        s += (min(__float_as_uint(v.x), 0x7f800000u) >> FMCW_K3_KEY_SHIFT) +
-             (min(__float_as_uint(v.y), 0x7f800000u) >> FMCW_K3_KEY_SHIFT) +
-             (min(__float_as_uint(v.z), 0x7f800000u) >> FMCW_K3_KEY_SHIFT) +
-             (min(__float_as_uint(v.w), 0x7f800000u) >> FMCW_K3_KEY_SHIFT);
+        k7[4 * u] = min(__float_as_uint(v.x), 0x7f800000u) >> FMCW_K3_KEY_SHIFT;
+        k7[4 * u + 1] = min(__float_as_uint(v.y), 0x7f800000u) >> FMCW_K3_KEY_SHIFT;
+        k7[4 * u + 2] = min(__float_as_uint(v.z), 0x7f800000u) >> FMCW_K3_KEY_SHIFT;
+        k7[4 * u + 3] = min(__float_as_uint(v.w), 0x7f800000u) >> FMCW_K3_KEY_SHIFT;
+        s += k7[4 * u] + k7[4 * u + 1] + k7[4 * u + 2] + k7[4 * u + 3];
       }
 #pragma unroll
       for (int x = 32; x >= 1; x >>= 1) s += (uint32_t)__shfl_xor((int)s, x, 64);
-      __syncthreads();  // the previous strip is done with cnt
+      __syncthreads();  // the previous strip is done with cnt and list
       if (threadIdx.x == 0) cnt[12] = 0u;
+      if (LV && threadIdx.x < 128) list[threadIdx.x] = 0u;
       __syncthreads();
       if (lane == 0) atomicAdd(&cnt[12], s);
       __syncthreads();
-      kb = (int)(cnt[12] / (uint32_t)(TR * NC)) - FMCW_K3_KEY_LOW;
+      const int mean7 = (int)(cnt[12] / (uint32_t)(TR * NC));
+      if constexpr (LV) {
+        const int h0 = mean7 - 64;  // histogram bin 0
+#pragma unroll
+        for (int i = 0; i < 16; ++i) atomicAdd(&list[min(max((int)k7[i] - h0, 0), 127)], 1u);
+        __syncthreads();
+        if (wv == 0) {
+          // bins 2 lane, 2 lane + 1: inclusive counts; the quantile bin = the first reaching p N
+          const uint32_t c0 = list[2 * lane], c1 = list[2 * lane + 1];
+          int tot;
+          const uint32_t ex = (uint32_t)wave_excl_scan((int)(c0 + c1), tot);
+          const uint32_t cum0 = ex + c0, cum1 = ex + c0 + c1;
+          const uint32_t na = (uint32_t)(FMCW_K3_LV_QA * (TR * NC) / 1000), nb = (uint32_t)(FMCW_K3_LV_QB * (TR * NC) / 1000);
+          const uint64_t ba0 = __ballot(cum0 >= na), ba1 = __ballot(cum1 >= na);
+          const uint64_t bb0 = __ballot(cum0 >= nb), bb1 = __ballot(cum1 >= nb);
+          // first bin: lane l's bin 2l if its cum0 qualifies, else 2l + 1
+          auto first_bin = [](uint64_t m0, uint64_t m1) {
+            const int l = __builtin_ctzll(m1);  // cum1 is reached by every qualifying lane
+            return (m0 >> l) & 1u ? 2 * l : 2 * l + 1;
+          };
+          if (lane == 0) {
+            cnt[14] = (uint32_t)first_bin(ba0, ba1);
+            cnt[15] = (uint32_t)first_bin(bb0, bb1);
+          }
+        }
+        __syncthreads();
+        // level keys QA <= QB (key16 units: key7 << 3) and the CUT bounds U = key16(fl(s_min lo(Q))), as
+        // the words lv_nibbles / cfar2d_screen_lv compare against
+        const uint32_t QA = (uint32_t)min(max((h0 + (int)cnt[14]) * 8, 1), 0x7f80);
+        const uint32_t QB = (uint32_t)min(max((h0 + (int)cnt[15]) * 8, 1), 0x7f80);
+        qa2 = QA | (QA << 16);
+        qb2 = QB | (QB << 16);
+        const uint32_t UA = key16(a.s_min * key_lo(QA)), UB = key16(a.s_min * key_lo(QB));
+        wa2 = ((UA | 0x8000u) - 1u) * 0x00010001u;
+        wb2 = ((UB | 0x8000u) - 1u) * 0x00010001u;
+      } else {
+        kb = mean7 - FMCW_K3_KEY_LOW;
+      }
     }
     for (int t = t_beg; t < t_end; ++t) {
       const int wt0 = t * WPB;                             // first wave tile of this step
@@ -478,14 +602,14 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
             v4[u] = 0.f;
             if (e4 < n4 && r >= 0 && r < ns) {
               v[u] = *reinterpret_cast<const float4*>(fm + (size_t)r * NC + d);
-              v4[u] = fm[(size_t)r * NC + ((d + 4) & (NC - 1))];
+              if constexpr (!LV) v4[u] = fm[(size_t)r * NC + ((d + 4) & (NC - 1))];
             }
           }
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int e4 = b + u * NT;
             const int x = e4 / (NC / 4), d = (e4 - x * (NC / 4)) * 4;
-            if (e4 < n4) put4(rr, x, d, v[u], v4[u], kb);
+            if (e4 < n4) put4(rr, x, d, v[u], v4[u]);
           }
         }
       } else {
@@ -497,7 +621,7 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
         for (int u = 0; u < 4; ++u) {
           const int e4 = tid + u * NT;
           const int i = e4 / (NC / 4), d = (e4 - i * (NC / 4)) * 4;
-          put4(rr, nr - TR + i, d, pre[u], pre4[u], kb);
+          put4(rr, nr - TR + i, d, pre[u], pre4[u]);
         }
       }
       if (t + 1 < t_end) {  // prefetch the next step's new rows r0 + TR + hr .. (zero past the map)
@@ -510,7 +634,7 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
           pre4[u] = 0.f;
           if (r < ns) {
             pre[u] = *reinterpret_cast<const float4*>(fm + (size_t)r * NC + d);
-            pre4[u] = fm[(size_t)r * NC + ((d + 4) & (NC - 1))];
+            if constexpr (!LV) pre4[u] = fm[(size_t)r * NC + ((d + 4) & (NC - 1))];
           }
         }
       }
@@ -527,13 +651,13 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
       };
       const bool tested = has_tile && r >= a.hr && r < ns - a.hr;
       if (tested) {
-        // cut_key7 of this lane's 16 CUTs, 4 per dword, from their staged key16 (an upper bound of
-        // the cut, as the candidate test uses: a higher threshold only keeps more cells).  No
-        // global re-read of the CUT cells: with 3 workgroups per CU their rows had often left L2
-        // again (K3 moved 1.8x the map bytes).
-        uint32_t Y[4];
-        const float inv_s = 1.0f / a.s_min;
-        {
+        if constexpr (LV) {
+          cand = cfar2d_screen_lv<NC, HR, GR>(rr, rlw, d0, need, wa2, wb2);
+        } else {
+          // cut_key7 of this lane's 16 CUTs, 4 per dword, from their staged key16 (an upper bound of
+          // the cut, as the candidate test uses: a higher threshold only keeps more cells)
+          uint32_t Y[4];
+          const float inv_s = 1.0f / a.s_min;
           const uint16_t* kr = rr.krow(rlw + a.hr) + k16idx(d0);
           const uint4 ka = *reinterpret_cast<const uint4*>(kr), kc = *reinterpret_cast<const uint4*>(kr + 8);
           const uint32_t kw[8] = {ka.x, ka.y, ka.z, ka.w, kc.x, kc.y, kc.z, kc.w};
@@ -543,11 +667,10 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
             Y[p] = cut_key7(key_hi(w0 & 0xffffu), inv_s, kb) | (cut_key7(key_hi(w0 >> 16), inv_s, kb) << 8) |
                    (cut_key7(key_hi(w1 & 0xffffu), inv_s, kb) << 16) | (cut_key7(key_hi(w1 >> 16), inv_s, kb) << 24);
           }
+          cand = cfar2d_screen7_generic<NC>(rr, rlw, d0, a, need, Y);
         }
-        if constexpr (HD > 0) cand = cfar2d_screen7<NC, HD, GD>(rr, rlw, d0, a, need, Y);
-        else cand = cfar2d_screen7_generic<NC>(rr, rlw, d0, a, need, Y);
 #ifdef FMCW_K3_ABLATE  // timing experiments (tools/k3_lab): 3 = staging + cut keys only, 1 = + screen
-        if (FMCW_K3_ABLATE == 3) cand = Y[0] == 12345u ? 1u : 0u;
+        if (FMCW_K3_ABLATE == 3) cand = 0u;
         if (FMCW_K3_ABLATE == 1) cand = cand == 0xffffu ? 1u : 0u;
 #endif
       }

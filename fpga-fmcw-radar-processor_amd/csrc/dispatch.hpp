@@ -51,7 +51,7 @@ struct Cfar2Info {
   Cfar2Fn fn;
   int TR;
 };
-Cfar2Info cfar2_info(uint32_t nc, int hd, int gd);  // inst_cfar2.hip
+Cfar2Info cfar2_info(uint32_t nc, int hd, int gd, int hr, int gr);  // inst_cfar2.hip
 size_t cfar2_smem(uint32_t nc, int hr);
 
 }  // namespace fmcw

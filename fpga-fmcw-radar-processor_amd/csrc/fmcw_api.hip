@@ -441,7 +441,7 @@ int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipS
   const int tile0 = (int)(frame0 * tiles_per_frame(h));
   if (c.cfar_kind == FMCW_CFAR_OS2D) {
     const Cfar2DArgs a = cfar2_args(c);
-    const Cfar2Info ci = cfar2_info(c.n_doppler, a.hd, a.gd);
+    const Cfar2Info ci = cfar2_info(c.n_doppler, a.hd, a.gd, a.hr, a.gr);
     // workgroup tiles (steps): 4 consecutive wave tiles of one frame; a strip is `steps` of them
     const int tpf = (int)((tiles_per_frame(h) + 3) / 4);
     const int steps = h->cfar2_steps ? std::min(h->cfar2_steps, tpf)
@@ -681,7 +681,7 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   if (c.cfar_kind == FMCW_CFAR_OS2D) {
     const Cfar2DArgs a = cfar2_args(c);
     h->cfar2d_smem = cfar2_smem(c.n_doppler, a.hr);
-    const Cfar2Info ci = cfar2_info(c.n_doppler, a.hd, a.gd);  // the kernel launch_cfar runs
+    const Cfar2Info ci = cfar2_info(c.n_doppler, a.hd, a.gd, a.hr, a.gr);  // the kernel launch_cfar runs
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(ci.fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)h->cfar2d_smem) != hipSuccess)
       (void)hipGetLastError();

@@ -3,16 +3,17 @@
 
 namespace fmcw {
 
-// the reference window (Doppler half extent 6, guard 2: os_cfar_2d as instantiated at
-// radar_core.vhd:376-382) gets the compile-time phase A; any other geometry the generic one
+// the reference window (range half extent 5, guard 1; Doppler half extent 6, guard 2: os_cfar_2d
+// as instantiated at radar_core.vhd:376-382) gets the compile-time level screen; any other
+// geometry the generic kernel (runtime window, pair screen)
 template <int N>
-static Cfar2Fn cfar2_fn(int hd, int gd) {
-  return (hd == 6 && gd == 2) ? k_cfar2d<N, 6, 2> : k_cfar2d<N, 0, 0>;
+static Cfar2Fn cfar2_fn(int hd, int gd, int hr, int gr) {
+  return (hd == 6 && gd == 2 && hr == 5 && gr == 1) ? k_cfar2d<N, 6, 2, 5, 1> : k_cfar2d<N, 0, 0>;
 }
 
-Cfar2Info cfar2_info(uint32_t nc, int hd, int gd) {
+Cfar2Info cfar2_info(uint32_t nc, int hd, int gd, int hr, int gr) {
   switch (nc) {
-#define C_(N) case N: return {cfar2_fn<N>(hd, gd), Cfar2DGeom<N>::TR};
+#define C_(N) case N: return {cfar2_fn<N>(hd, gd, hr, gr), Cfar2DGeom<N>::TR};
     C_(32) C_(64) C_(128) C_(256) C_(512) C_(1024)
 #undef C_
   }

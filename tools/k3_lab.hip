@@ -109,9 +109,9 @@ int main(int argc, char** argv) {
   a.compat = 0;
   a.s_min = 2.f;
   std::vector<Var> vars;
-  vars.push_back({"k_cfar2d (production)", reinterpret_cast<const void*>(k_cfar2d<NC, 6, 2>),
+  vars.push_back({"k_cfar2d (production)", reinterpret_cast<const void*>(k_cfar2d<NC, 6, 2, 5, 1>),
                   cfar2d_smem_bytes<NC>(a.hr), [&](int grid, size_t smem, int n_strips, int steps, DetSink sink) {
-                    hipLaunchKernelGGL((k_cfar2d<NC, 6, 2>), dim3(grid), dim3(256), smem, 0, map, ns, n_strips,
+                    hipLaunchKernelGGL((k_cfar2d<NC, 6, 2, 5, 1>), dim3(grid), dim3(256), smem, 0, map, ns, n_strips,
                                        steps, 0, 0, a, sink);
                   }});
 #ifdef K3_LAB_PREV
