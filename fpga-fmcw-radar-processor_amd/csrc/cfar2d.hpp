@@ -33,6 +33,18 @@ struct Cfar2DArgs {
   int compat;          // FMCW_COMPAT_CFAR: 17-bit integer cells, integer mean and brackets
 };
 
+// The candidate list of one 2-D CFAR launch (capacity: every cell of the launch, so it cannot
+// overflow): cell[i] = (frame in the launch x ns + range) x NC + doppler, runs of one wave tile in
+// cell order; thr[i] = the threshold of a detection, -1 for a rejected candidate (k_cfar2d_decide);
+// tiles[] = the wave tiles with candidates; ctr[0] = candidates, ctr[1] = such tiles (zeroed before
+// the launch).
+struct Cfar2Cands {
+  uint32_t* cell;
+  float* thr;
+  uint32_t* tiles;
+  uint32_t* ctr;
+};
+
 // 7-bit keys.  key(v) = clamp((bits(v) >> SH) - base, 0, 127) for a non-negative fp32 cell v:
 // 2^(23 - SH) levels per octave (16 at SH = 19) over a 128-level window that starts `base`
 // levels up; base is set per strip from the mean level of its first step's cells minus LOW
@@ -437,7 +449,8 @@ __device__ __forceinline__ uint32_t wave_select_kth(uint32_t ka, uint32_t kb, ui
 template <int NC, int HD, int GD, int HR = 0, int GR = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FMCW_K3_WAVES)))
 k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int frame0, int tile0, Cfar2DArgs a,
-         DetSink sink) {
+         DetSink sink, Cfar2Cands cands) {
+  (void)frame0;
   constexpr bool LV = HD > 0;
   static_assert(!LV || (HD == 6 && GD == 2 && HR >= 1), "the level screen is built for the reference window");
   using Gm = Cfar2DGeom<NC>;
@@ -448,11 +461,6 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
 
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // this lane's two reference cells (index lane and lane + 64 of the fixed order)
-  int dra, dda, drb, ddb;
-  cfar2d_ref_offset(a, lane, dra, dda);
-  cfar2d_ref_offset(a, lane + 64, drb, ddb);
-  const bool oka = lane < a.n_ref, okb = lane + 64 < a.n_ref;
   const int need = a.n_ref - a.rank;
   const int wt_per_frame = ns / WR;                      // wave tiles per frame
   const int wg_per_frame = (wt_per_frame + WPB - 1) / WPB;
@@ -503,11 +511,6 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
     const int f = g % nf;
     const int t_beg = (g / nf) * steps, t_end = min(t_beg + steps, wg_per_frame);
     const float* fm = map + (size_t)f * ns * NC;
-    // an exact cell of the frame (as staged: clamped at 0, or 17-bit integer in compat mode)
-    auto cell = [&](int r, int d) {
-      const float v = fm[(size_t)r * NC + d];
-      return a.compat ? q17(v) : nonneg(v);
-    };
     RowRing rr{tile, keys, 0, nr, RB, Gm::KRS};
     float4 pre[4];
     float pre4[4];
@@ -730,87 +733,140 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
       if (FMCW_K3_ABLATE == 2) n_cand = 0u;
 #endif
       const int wtile = tile0 + f * wt_per_frame + wt0 + wv;
-      if (n_cand == 0u) {  // (most steps) no candidate: the tiles are empty, phase B's barriers skipped
-        if (has_tile && lane == 0) {
-          sink.wg_base[wtile] = (uint32_t)wtile * sink.slot_cap;
-          sink.wg_count[wtile] = 0u;
-        }
-        continue;
-      }
-
-      // ---- Phase B: one whole wave per candidate cell, on the exact fp32 cells of the map.
-      // Lanes hold refs l and l + 64 of the fixed order; the mean is the fixed fp32 halving
-      // tree; the scale bracket comes from ballot counts.
-      auto refs_of = [&](int trow, int d, float& va, float& vb) {
-        va = oka ? cell(r0 + trow + dra, (d + dda) & (NC - 1)) : 0.f;
-        vb = okb ? cell(r0 + trow + drb, (d + ddb) & (NC - 1)) : 0.f;
-      };
-      auto scale_of = [&](float va, float vb) -> float {
-        float sum = va + vb;
-#pragma unroll
-        for (int x = 32; x >= 1; x >>= 1) sum += __shfl_xor(sum, x, 64);
-        if (a.override_) return (float)a.override_;
-        float half, hi;
-        if (a.compat) {
-          // integer cells < 2^17, <= 128 of them: every partial sum < 2^24 is exact in fp32.
-          // mean = floor(sum / N_REF) (os_cfar_2d.vhd:189); the bracket add is 17 bits wide (:193)
-          const uint32_t mean = (uint32_t)sum / (uint32_t)a.n_ref;
-          half = (float)(mean >> 1);
-          hi = (float)((mean + (mean >> 1)) & kQ17Mask);
-        } else {
-          const float mean = sum / (float)a.n_ref;
-          half = mean * 0.5f;
-          hi = mean + half;
-        }
-        const int n_hi = __popcll(__ballot(oka && va > hi)) + __popcll(__ballot(okb && vb > hi));
-        const int n_lo = __popcll(__ballot(oka && va < half)) + __popcll(__ballot(okb && vb < half));
-        return (n_hi >= need) ? a.sc_max : (n_lo >= a.rank + 1) ? a.sc_min : a.sc_nom;
-      };
-
-      // Pass 1: decide every candidate; the four waves take the round's entries in turn
-      aux[threadIdx.x] = 0u;
-      coop_rounds(cand, cnt + 4, list, nullptr, 0u, [&](int n) {
-        for (int j = wv; j < n; j += WPB) {
-          int trow, d;
-          const uint32_t e = list[j];
-          cell_of(e, trow, d);
-          const float cut = cell(r0 + trow, d);
-          float va, vb;
-          refs_of(trow, d, va, vb);
-          const float sc = scale_of(va, vb);
-          const int n_ge = __popcll(__ballot(oka && sc * va >= cut)) + __popcll(__ballot(okb && sc * vb >= cut));
-          if (n_ge < need && lane == 0) atomicOr(&aux[e >> 4], 1u << (e & 15u));
-        }
-      });
-      const uint32_t detw = aux[threadIdx.x];
-      int total;
-      const int dx = wave_excl_scan(__popc(detw), total);
-      const uint32_t base = has_tile ? det_reserve_wave(sink, wtile, total) : 0u;
-      __syncthreads();  // aux now carries sink positions
-
-      // Pass 2: exact ranked value (k-th smallest) of each detection by a pivoting select on the
-      // bit patterns (cells are non-negative: unsigned order == value order), then the record
-      coop_rounds(detw, cnt + 8, list, aux, base + (uint32_t)dx, [&](int n) {
-        for (int j = wv; j < n; j += WPB) {
-          int trow, d;
-          cell_of(list[j], trow, d);
-          const uint32_t slot = aux[j];
-          float va, vb;
-          refs_of(trow, d, va, vb);
-          const float sc = scale_of(va, vb);
-          const uint32_t ranked = wave_select_kth(oka ? __float_as_uint(va) : 0u, okb ? __float_as_uint(vb) : 0u,
-                                                  __ballot(oka), __ballot(okb), a.rank);
-          if (lane == 0 && slot < sink.cap) {
-            fmcw_det dd;
-            dd.frame = (uint32_t)(frame0 + f);
-            dd.range = (uint16_t)(r0 + trow);
-            dd.doppler = (uint16_t)d;
-            dd.mag = cell(r0 + trow, d);
-            dd.threshold = sc * __uint_as_float(ranked);
-            sink.scratch[slot] = dd;
+      // ---- Emission: the wave tile's candidates, in (range, doppler) order, go to the launch's
+      // candidate list as one contiguous run (k_cfar2d_decide decides them, k_cfar2d_emit writes
+      // the tile's records); (wg_base, wg_count) = (run start, run length) until then.  An empty
+      // tile is final here.
+      if (has_tile) {
+        uint32_t mine = 0u;
+        if (n_cand != 0u) mine = cand;  // bits of this lane's candidates (cand: aux after the test)
+        int k_w;
+        const int ex = wave_excl_scan(__popc(mine), k_w);
+        if (k_w == 0) {
+          if (lane == 0) {
+            sink.wg_base[wtile] = (uint32_t)wtile * sink.slot_cap;
+            sink.wg_count[wtile] = 0u;
           }
+        } else {
+          uint32_t p0 = 0u;
+          if (lane == 0) {
+            p0 = atomicAdd(&cands.ctr[0], (uint32_t)k_w);
+            cands.tiles[atomicAdd(&cands.ctr[1], 1u)] = (uint32_t)wtile;
+            sink.wg_base[wtile] = p0;
+            sink.wg_count[wtile] = (uint32_t)k_w;
+          }
+          p0 = (uint32_t)__shfl((int)p0, 0, 64);
+          const uint32_t cbase = ((uint32_t)f * (uint32_t)ns + (uint32_t)r) * (uint32_t)NC + (uint32_t)d0;
+          uint32_t o = p0 + (uint32_t)ex;
+          for (uint32_t m = mine; m; m &= m - 1, ++o) cands.cell[o] = cbase + (uint32_t)__builtin_ctz(m);
         }
-      });
+      }
     }  // steps
   }    // strips
+}
+
+// ---- K3b: the exact decision of every candidate of a launch, one whole wave per candidate, all
+// waves of the GPU sharing the list (round 4: inside k_cfar2d the 4 waves of the workgroup that
+// met a target's rows decided its dozens of candidates one after the other, and that step set the
+// critical path of the launch).  On the exact fp32 cells of the map: lanes hold refs l and l + 64 of
+// the fixed order (dr ascending outer, dd ascending inner, guard block skipped; oracle
+// cfar2d_offsets); the mean is the fixed fp32 halving tree (one add, then xor-shuffles 32..1 ==
+// oracle tree_sum_f32); the scale bracket comes from ballot counts (ranked > M <=> #{ref > M} >=
+// n_ref - k; os_cfar_2d.vhd:189-213); detect <=> #{fl(s ref) >= cut} < n_ref - k; a detection's
+// ranked value (k-th smallest) by the pivoting select, threshold = fl(s ranked) (dbg_threshold).
+template <int NC>
+__global__ void __launch_bounds__(256)
+k_cfar2d_decide(const float* __restrict__ map, int ns, Cfar2DArgs a, Cfar2Cands cands) {
+  const int lane = threadIdx.x & 63;
+  int dra, dda, drb, ddb;
+  cfar2d_ref_offset(a, lane, dra, dda);
+  cfar2d_ref_offset(a, lane + 64, drb, ddb);
+  const bool oka = lane < a.n_ref, okb = lane + 64 < a.n_ref;
+  const int need = a.n_ref - a.rank;
+  const uint32_t n = cands.ctr[0];
+  const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+  auto cell = [&](uint32_t i) {
+    const float v = map[i];
+    return a.compat ? q17(v) : nonneg(v);
+  };
+  for (uint32_t i = w0; i < n; i += nw) {
+    const uint32_t c = cands.cell[i];                     // (f ns + r) NC + d
+    const uint32_t fr = c / (uint32_t)NC, d = c & (uint32_t)(NC - 1);  // fr = f ns + r
+    const float cut = cell(c);
+    // refs: rows r + dr stay inside the frame (a CUT row has its whole range extent inside it)
+    const float va = oka ? cell((fr + dra) * (uint32_t)NC + ((d + dda) & (uint32_t)(NC - 1))) : 0.f;
+    const float vb = okb ? cell((fr + drb) * (uint32_t)NC + ((d + ddb) & (uint32_t)(NC - 1))) : 0.f;
+    float sum = va + vb;
+#pragma unroll
+    for (int x = 32; x >= 1; x >>= 1) sum += __shfl_xor(sum, x, 64);
+    float sc = (float)a.override_;
+    if (!a.override_) {
+      float half, hi;
+      if (a.compat) {
+        // integer cells < 2^17, <= 128 of them: every partial sum < 2^24 is exact in fp32.
+        // mean = floor(sum / N_REF) (os_cfar_2d.vhd:189); the bracket add is 17 bits wide (:193)
+        const uint32_t mean = (uint32_t)sum / (uint32_t)a.n_ref;
+        half = (float)(mean >> 1);
+        hi = (float)((mean + (mean >> 1)) & kQ17Mask);
+      } else {
+        const float mean = sum / (float)a.n_ref;
+        half = mean * 0.5f;
+        hi = mean + half;
+      }
+      const int n_hi = __popcll(__ballot(oka && va > hi)) + __popcll(__ballot(okb && vb > hi));
+      const int n_lo = __popcll(__ballot(oka && va < half)) + __popcll(__ballot(okb && vb < half));
+      sc = (n_hi >= need) ? a.sc_max : (n_lo >= a.rank + 1) ? a.sc_min : a.sc_nom;
+    }
+    const int n_ge = __popcll(__ballot(oka && sc * va >= cut)) + __popcll(__ballot(okb && sc * vb >= cut));
+    float thr = -1.f;
+    if (n_ge < need) {  // uniform
+      const uint32_t ranked = wave_select_kth(oka ? __float_as_uint(va) : 0u, okb ? __float_as_uint(vb) : 0u,
+                                              __ballot(oka), __ballot(okb), a.rank);
+      thr = sc * __uint_as_float(ranked);
+    }
+    if (lane == 0) cands.thr[i] = thr;
+  }
+}
+
+// ---- K3c: per wave tile with candidates, its detections in order into the sink (det_reserve_wave:
+// the tile's slot, or the overflow region), 64 candidates per round.
+template <int NC>
+__global__ void __launch_bounds__(256)
+k_cfar2d_emit(const float* __restrict__ map, int ns, int frame0, Cfar2DArgs a, Cfar2Cands cands, DetSink sink) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nt = cands.ctr[1];
+  const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+  for (uint32_t ti = w0; ti < nt; ti += nw) {
+    const int tile = (int)cands.tiles[ti];
+    const uint32_t p0 = sink.wg_base[tile], k = sink.wg_count[tile];  // the candidate run (k_cfar2d)
+    int total = 0;
+    for (uint32_t j0 = 0; j0 < k; j0 += 64) {
+      const bool det = j0 + lane < k && cands.thr[p0 + j0 + lane] >= 0.f;
+      total += (int)__popcll(__ballot(det));
+    }
+    const uint32_t base = det_reserve_wave(sink, tile, total);
+    uint32_t o = base;
+    for (uint32_t j0 = 0; j0 < k; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      const float thr = j < k ? cands.thr[p0 + j] : -1.f;
+      const uint64_t bal = __ballot(thr >= 0.f);
+      if (thr >= 0.f) {
+        const uint32_t slot = o + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        if (slot < sink.cap) {
+          const uint32_t c = cands.cell[p0 + j];
+          const uint32_t fr = c / (uint32_t)NC;
+          const float v = map[c];
+          fmcw_det dd;
+          dd.frame = (uint32_t)frame0 + fr / (uint32_t)ns;
+          dd.range = (uint16_t)(fr % (uint32_t)ns);
+          dd.doppler = (uint16_t)(c & (uint32_t)(NC - 1));
+          dd.mag = a.compat ? q17(v) : nonneg(v);
+          dd.threshold = thr;
+          sink.scratch[slot] = dd;
+        }
+      }
+      o += (uint32_t)__popcll(bal);
+    }
+  }
 }

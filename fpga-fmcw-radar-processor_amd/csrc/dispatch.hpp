@@ -46,10 +46,14 @@ inline DopplerInfo doppler_info(uint32_t nc, int mti = FMCW_MTI_OFF, bool h16 = 
 // ---- stand-alone 1-D CFAR (fmcw_cfar) and K3 2-D CFAR ---------------------------------------
 using Cfar1Fn = void (*)(const float*, int, int, int, int, Cfar1DArgs, DetSink);
 Cfar1Fn cfar1_fn(uint32_t nc);  // inst_doppler.hip
-using Cfar2Fn = void (*)(const float*, int, int, int, int, int, Cfar2DArgs, DetSink);
+using Cfar2Fn = void (*)(const float*, int, int, int, int, int, Cfar2DArgs, DetSink, Cfar2Cands);
+using Cfar2DecideFn = void (*)(const float*, int, Cfar2DArgs, Cfar2Cands);
+using Cfar2EmitFn = void (*)(const float*, int, int, Cfar2DArgs, Cfar2Cands, DetSink);
 struct Cfar2Info {
-  Cfar2Fn fn;
+  Cfar2Fn fn;           // K3a k_cfar2d: screen, candidate test, the candidate list
   int TR;
+  Cfar2DecideFn decide; // K3b k_cfar2d_decide
+  Cfar2EmitFn emit;     // K3c k_cfar2d_emit
 };
 Cfar2Info cfar2_info(uint32_t nc, int hd, int gd, int hr, int gr);  // inst_cfar2.hip
 size_t cfar2_smem(uint32_t nc, int hr);

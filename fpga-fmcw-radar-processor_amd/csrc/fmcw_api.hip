@@ -62,12 +62,16 @@ k_det_scan_top(uint32_t* __restrict__ block_sum, int nb, uint32_t* __restrict__ 
   }
 }
 
-// Start of a call: the handle's detection counters and the caller's status words, zeroed by one
-// launch (two hipMemsetAsync fills cost ~12 us per call, 1 % of a config-2 step).
-__global__ void k_zero_words(uint32_t* __restrict__ a, int na, uint32_t* __restrict__ b, int nb) {
-  const int i = threadIdx.x;
-  if (a && i < na) a[i] = 0u;
-  if (b && i < nb) b[i] = 0u;
+// Start of a call: the handle's detection counters, the caller's status words and the 2-D CFAR
+// launches' candidate counters, zeroed by one launch (two hipMemsetAsync fills cost ~12 us per
+// call, 1 % of a config-2 step).
+__global__ void k_zero_words(uint32_t* __restrict__ a, int na, uint32_t* __restrict__ b, int nb,
+                             uint32_t* __restrict__ c, int nc) {
+  for (int i = threadIdx.x; i < max(na, max(nb, nc)); i += blockDim.x) {
+    if (a && i < na) a[i] = 0u;
+    if (b && i < nb) b[i] = 0u;
+    if (c && i < nc) c[i] = 0u;
+  }
 }
 
 // One lane per tile; a tile with more than 8 detections (a target's row) is copied by the
@@ -201,6 +205,14 @@ struct fmcw_handle {
   size_t inter_bytes = 0;               // h->inter (chunk frames of the K1 -> K2 spectrum)
   int cfar2_steps = 0;                  // 2-D CFAR steps per strip (0 = cost model; FMCW_PARAM_CFAR2D_STEPS)
   int cfar2_steps_last = 0;             // the strip length of the last 2-D CFAR launch (FMCW_INFO_CFAR2D_STEPS)
+  // 2-D CFAR candidate lists (cfar2d.hpp Cfar2Cands): room for every cell of k3_frames frames, and
+  // a counter pair per K3 launch of a call (k3_launches of them, zeroed with the status words)
+  uint32_t* cand_cell = nullptr;
+  float* cand_thr = nullptr;
+  uint32_t* cand_tiles = nullptr;
+  uint32_t* k3_ctr = nullptr;
+  int k3_frames = 0, k3_launches = 0;
+  int k3_launch_idx = 0;                // launches of the current call so far
   uint32_t last_status[2] = {0, 0};     // fmcw_process: status words 2, 3 of its last call
   // profiling
   bool profiling = false;
@@ -433,6 +445,8 @@ int cfar2_steps_model(int nf, int tpf, int grid, int tr, int hr) {
 }
 
 constexpr size_t kCfar2Batch = 16;  // frames per 2-D CFAR launch on the caller's map (at least)
+constexpr int kCfar2DecideGrid = 1024;  // K3b workgroups (4 waves each, one candidate per wave at a time)
+constexpr int kCfar2EmitGrid = 256;     // K3c workgroups (one wave tile per wave at a time)
 
 // The CFAR launcher shared by fmcw_enqueue (map just produced by K2) and fmcw_cfar.
 int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipStream_t s) {
@@ -442,17 +456,31 @@ int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipS
   if (c.cfar_kind == FMCW_CFAR_OS2D) {
     const Cfar2DArgs a = cfar2_args(c);
     const Cfar2Info ci = cfar2_info(c.n_doppler, a.hd, a.gd, a.hr, a.gr);
-    // workgroup tiles (steps): 4 consecutive wave tiles of one frame; a strip is `steps` of them
-    const int tpf = (int)((tiles_per_frame(h) + 3) / 4);
-    const int steps = h->cfar2_steps ? std::min(h->cfar2_steps, tpf)
-                                     : cfar2_steps_model(nf, tpf, h->grid_cfar, doppler_info(c.n_doppler).WR * 4, a.hr);
-    const int n_strips = nf * ((tpf + steps - 1) / steps);
-    const int grid = std::min(n_strips, h->grid_cfar);
-    h->cfar2_steps_last = steps;
-    ProfScope ps(h, FMCW_K_CFAR2D, s);
-    hipLaunchKernelGGL(ci.fn, dim3(grid), dim3(256), h->cfar2d_smem, s, map_chunk, (int)c.n_range,
-                       n_strips, steps, frame0, tile0, a, sink);
-    return check_launch("k_cfar2d");
+    const size_t frame_px = (size_t)c.n_range * c.n_doppler;
+    // pieces of at most k3_frames frames (the candidate lists' capacity), each its own K3a/b/c
+    for (int p0 = 0; p0 < nf; p0 += h->k3_frames) {
+      const int np = std::min(h->k3_frames, nf - p0);
+      if (h->k3_launch_idx >= h->k3_launches) return fail(FMCW_EINVAL, "2-D CFAR: launch counter slots exhausted");
+      Cfar2Cands cands{h->cand_cell, h->cand_thr, h->cand_tiles, h->k3_ctr + 2 * h->k3_launch_idx++};
+      const float* mp = map_chunk + (size_t)p0 * frame_px;
+      // workgroup tiles (steps): 4 consecutive wave tiles of one frame; a strip is `steps` of them
+      const int tpf = (int)((tiles_per_frame(h) + 3) / 4);
+      const int steps = h->cfar2_steps ? std::min(h->cfar2_steps, tpf)
+                                       : cfar2_steps_model(np, tpf, h->grid_cfar, doppler_info(c.n_doppler).WR * 4, a.hr);
+      const int n_strips = np * ((tpf + steps - 1) / steps);
+      const int grid = std::min(n_strips, h->grid_cfar);
+      h->cfar2_steps_last = steps;
+      ProfScope ps(h, FMCW_K_CFAR2D, s);
+      hipLaunchKernelGGL(ci.fn, dim3(grid), dim3(256), h->cfar2d_smem, s, mp, (int)c.n_range, n_strips, steps,
+                         frame0 + p0, tile0 + (int)(p0 * tiles_per_frame(h)), a, sink, cands);
+      if (int rc = check_launch("k_cfar2d")) return rc;
+      // K3b / K3c: fixed grids that read the candidate counts on the device (no host round trip)
+      hipLaunchKernelGGL(ci.decide, dim3(kCfar2DecideGrid), dim3(256), 0, s, mp, (int)c.n_range, a, cands);
+      hipLaunchKernelGGL(ci.emit, dim3(kCfar2EmitGrid), dim3(256), 0, s, mp, (int)c.n_range, frame0 + p0, a, cands,
+                         sink);
+      if (int rc = check_launch("k_cfar2d_decide / _emit")) return rc;
+    }
+    return FMCW_OK;
   }
   // 1-D on a caller map (fmcw_cfar); inside fmcw_enqueue the 1-D CFAR is fused into K2
   const DopplerInfo di = doppler_info(c.n_doppler);
@@ -645,7 +673,22 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   // >= one fp32 frame: fmcw_range_ct writes the fp32 spectrum through it whatever spectrum_dtype
   h->inter_bytes = std::max((size_t)h->chunk * frame_inter, (size_t)c.n_rx * c.n_range * c.n_doppler * sizeof(float2));
   ALLOC(h->inter, h->inter_bytes);
-  if (c.cfar_kind == FMCW_CFAR_OS2D) ALLOC(h->lin_scratch, (size_t)h->chunk * c.n_range * c.n_doppler * sizeof(float));
+  if (c.cfar_kind == FMCW_CFAR_OS2D) {
+    ALLOC(h->lin_scratch, (size_t)h->chunk * c.n_range * c.n_doppler * sizeof(float));
+    // candidate lists for K3 launches of up to k3_frames frames (fmcw_enqueue's batches: >= 16
+    // frames, ending on a chunk boundary): every cell may be a candidate, so they cannot overflow
+    h->k3_frames = (int)std::min<size_t>(c.max_frames, kCfar2Batch + h->chunk);
+    const size_t cells = (size_t)h->k3_frames * c.n_range * c.n_doppler;
+    if (cells > 0xffffffffu) return cleanup(fail(FMCW_EINVAL, "2-D CFAR launch too large for 32-bit cell indices"));
+    // K3 launches per call: one per chunk at most (map-less calls run it on each chunk's scratch),
+    // else one per >= 16-frame batch, or one per k3_frames piece (fmcw_cfar)
+    const size_t minb = std::min<size_t>(h->chunk, kCfar2Batch);
+    h->k3_launches = (int)((c.max_frames + minb - 1) / minb + (c.max_frames + h->k3_frames - 1) / h->k3_frames + 2);
+    ALLOC(h->cand_cell, cells * sizeof(uint32_t));
+    ALLOC(h->cand_thr, cells * sizeof(float));
+    ALLOC(h->cand_tiles, (size_t)h->k3_frames * tiles_per_frame(h) * sizeof(uint32_t));
+    ALLOC(h->k3_ctr, (size_t)2 * h->k3_launches * sizeof(uint32_t));
+  }
   h->n_wg_max = (size_t)c.max_frames * tiles_per_frame(h);
   {
     // Each tile owns a slot of 1/32 of its cells (a 3 % detection density, far above any
@@ -709,7 +752,8 @@ int fmcw_destroy(fmcw_handle* h) {
   hipSetDevice(h->cfg.device_id);
   void* ptrs[] = {h->win_r, h->win_d, h->inter, h->lin_scratch, h->det_scratch, h->counter,
                   h->n_dets_tmp, h->wg_base, h->wg_count, h->wg_off, h->block_sum,
-                  h->stage_cube, h->stage_map, h->stage_dets};
+                  h->stage_cube, h->stage_map, h->stage_dets, h->cand_cell, h->cand_thr,
+                  h->cand_tiles, h->k3_ctr};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& pe : h->pending) {
@@ -741,8 +785,9 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
   uint32_t* const status = n_dets_dev ? n_dets_dev + 2 : nullptr;
   int rc;
   if (c.cfar_kind != FMCW_CFAR_NONE || n_dets_dev) {
-    hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(64), 0, s, c.cfar_kind != FMCW_CFAR_NONE ? h->counter : nullptr, 2,
-                       n_dets_dev, FMCW_STATUS_WORDS);
+    hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(256), 0, s, c.cfar_kind != FMCW_CFAR_NONE ? h->counter : nullptr, 2,
+                       n_dets_dev, FMCW_STATUS_WORDS, h->k3_ctr, 2 * h->k3_launches);
+    h->k3_launch_idx = 0;
     if ((rc = check_launch("k_zero_words"))) return rc;
   }
 
@@ -897,8 +942,10 @@ int fmcw_cfar(fmcw_handle* h, const float* map, size_t n_frames, fmcw_det* dets,
   if (n_frames < 1 || n_frames > c.max_frames) return fail(FMCW_EINVAL, "n_frames out of range");
   HIP_TRY(hipSetDevice(c.device_id));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(64), 0, s, h->counter, 2, n_dets_dev, FMCW_STATUS_WORDS);
+  hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(256), 0, s, h->counter, 2, n_dets_dev, FMCW_STATUS_WORDS, h->k3_ctr,
+                     2 * h->k3_launches);
   if (int rc0 = check_launch("k_zero_words")) return rc0;
+  h->k3_launch_idx = 0;
   int rc = launch_cfar(h, map, (int)n_frames, 0, s);
   if (rc) return rc;
   return launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, s);
@@ -929,6 +976,15 @@ int fmcw_get_info(fmcw_handle* h, int key, int64_t* value) {
     case FMCW_INFO_WINDOW_SATURATIONS: *value = h->last_status[0]; return FMCW_OK;
     case FMCW_INFO_WORD_SATURATIONS: *value = h->last_status[1]; return FMCW_OK;
     case FMCW_INFO_CFAR2D_STEPS: *value = h->cfar2_steps_last; return FMCW_OK;
+#if FMCW_LAB
+    case 100:  // FMCW_K3_COUNT builds: 2-D CFAR screen survivors / candidates since fmcw_cfar's zeroing
+    case 101: {
+      uint32_t w[4] = {0, 0, 0, 0};
+      HIP_TRY(hipMemcpy(w, h->counter, sizeof w, hipMemcpyDeviceToHost));
+      *value = w[key - 98];
+      return FMCW_OK;
+    }
+#endif
   }
   return fail(FMCW_EINVAL, "fmcw_get_info: unknown key %d", key);
 }

@@ -13,7 +13,7 @@ static Cfar2Fn cfar2_fn(int hd, int gd, int hr, int gr) {
 
 Cfar2Info cfar2_info(uint32_t nc, int hd, int gd, int hr, int gr) {
   switch (nc) {
-#define C_(N) case N: return {cfar2_fn<N>(hd, gd, hr, gr), Cfar2DGeom<N>::TR};
+#define C_(N) case N: return {cfar2_fn<N>(hd, gd, hr, gr), Cfar2DGeom<N>::TR, k_cfar2d_decide<N>, k_cfar2d_emit<N>};
     C_(32) C_(64) C_(128) C_(256) C_(512) C_(1024)
 #undef C_
   }

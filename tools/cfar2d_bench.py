@@ -10,6 +10,7 @@ usage: python tools/cfar2d_bench.py [--workloads c3,c5] [--iters 20] [--ovr 0,7]
 import argparse
 import hashlib
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -53,8 +54,19 @@ def main():
         for ovr in [int(x) for x in a.ovr.split(",")]:
             with RadarCore(N_RANGE=ns, N_DOPPLER=nc, N_RX=nrx, in_dtype=g["dtype"], cfar="os2d",
                            max_frames=F, cfar_scale_ovr=ovr) as core:
+                cnt = {}
+                if os.environ.get("FMCW_K3_COUNTS"):  # a FMCW_LAB + FMCW_K3_COUNT variant library
+                    import ctypes as C
+                    def rd(k):
+                        v = C.c_int64(0)
+                        core._lib.fmcw_get_info(core._h, k, C.byref(v))
+                        return v.value
+                    s0, c0 = rd(100), rd(101)
                 core.cfar(rd_map, F, dets, cap, nd, stream=stream)  # warm-up
                 torch.cuda.synchronize()
+                if os.environ.get("FMCW_K3_COUNTS"):
+                    cnt = {"screen_survivors": rd(100) - s0, "candidates": rd(101) - c0,
+                           "cells": F * ns * nc}
                 core.set_profiling(True)
                 core.reset_kernel_times()
                 for _ in range(a.iters):
@@ -68,7 +80,7 @@ def main():
                                   round(1e3 * ms / max(1, calls), 2), "launches": calls,
                                   "frames_per_launch": F * a.iters / max(1, calls),
                                   "us_per_frame": round(1e3 * ms / (F * a.iters), 2),
-                                  "n_dets": n, "dets_sha1": h}), flush=True)
+                                  "n_dets": n, "dets_sha1": h, **cnt}), flush=True)
         del rd_map, dets
 
 

@@ -2,7 +2,8 @@
 // BASELINE config 5's map geometry (8192 range x 1024 Doppler, 2-D CFAR with the reference
 // window of rtl/src/os_cfar_2d.vhd as instantiated at radar_core.vhd:376-382).
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -o tools/k3_lab tools/k3_lab.hip
-// Run:   tools/k3_lab [frames=16] [reps=5] [ns=8192]
+// Run:   tools/k3_lab [frames=16] [reps=5] [ns=8192] [nc=1024] [nrx=1]   (nc 1024 / 512 / 256; nrx > 1:
+//        the cells are the non-coherent sum over nrx complex-Gaussian channels, as config 3's NCI map)
 // Synthetic map: Rayleigh noise (|complex Gaussian|) plus point targets with Hamming-like
 // sidelobes; every variant's detection list (per tile: count + records) must equal the
 // production kernel's, and each variant's average launch time is reported.
@@ -38,8 +39,6 @@ using namespace fmcw;
     }                                                                                      \
   } while (0)
 
-constexpr int NC = 1024;
-
 __device__ uint32_t hash32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7feb352dU;
@@ -48,20 +47,24 @@ __device__ uint32_t hash32(uint32_t x) {
   x ^= x >> 16;
   return x;
 }
-// Rayleigh magnitude (sigma 1000) + targets: every 512th range row has a target at Doppler
-// (row * 37) % NC of amplitude 1e6 with a 3 x 5 neighbourhood at 1e4
-__global__ void k_fill_map(float* m, int ns, size_t n) {
+// Rayleigh magnitude (sigma 1000; nrx > 1: sqrt of the sum of nrx squared Rayleigh cells, the NCI
+// map) + targets: every 512th range row has a target at Doppler (row * 37) % nc of amplitude 1e6
+// with a 3 x 5 neighbourhood at 1e4
+__global__ void k_fill_map(float* m, int ns, int nc, int nrx, size_t n) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t h1 = hash32((uint32_t)i * 2u + 1u), h2 = hash32((uint32_t)i * 2u + 2u);
-    const float u1 = ((float)(h1 >> 8) + 0.5f) / 16777216.f, u2 = (float)(h2 >> 8) / 16777216.f;
-    float v = 1000.f * sqrtf(-2.f * logf(u1));  // Rayleigh: |N(0,1) + i N(0,1)|
-    (void)u2;
-    const int d = (int)(i % NC);
-    const size_t rr = i / NC;
+    float p = 0.f;
+    for (int x = 0; x < nrx; ++x) {
+      const uint32_t h1 = hash32((uint32_t)i * 8u + 2u * x + 1u);
+      const float u1 = ((float)(h1 >> 8) + 0.5f) / 16777216.f;
+      p += -2.f * logf(u1);  // |N(0,1) + i N(0,1)|^2
+    }
+    float v = 1000.f * sqrtf(p);
+    const int d = (int)(i % nc);
+    const size_t rr = i / nc;
     const int r = (int)(rr % ns);
     const int rt = (r + 2) / 512 * 512;  // nearest target row
-    const int dt = (rt * 37) % NC;
-    const int dr = r - rt, dd = ((d - dt + NC + NC / 2) % NC) - NC / 2;
+    const int dt = (rt * 37) % nc;
+    const int dr = r - rt, dd = ((d - dt + nc + nc / 2) % nc) - nc / 2;
     if (rt > 0 && rt < ns && abs(dr) <= 1 && abs(dd) <= 2) v = (dr == 0 && dd == 0) ? 1e6f : 1e4f;
     m[i] = v;
   }
@@ -71,7 +74,7 @@ struct Var {
   std::string name;
   const void* fn;
   size_t smem;
-  std::function<void(int grid, size_t smem, int n_strips, int steps, DetSink sink)> launch;
+  std::function<void(int grid, size_t smem, int n_strips, int steps, DetSink sink, Cfar2Cands cands)> launch;
 };
 
 int steps_model(int nf, int tpf, int grid, int tr, int hr) {  // = fmcw_api.hip cfar2_steps_model
@@ -89,10 +92,8 @@ int steps_model(int nf, int tpf, int grid, int tr, int hr) {  // = fmcw_api.hip 
   return best;
 }
 
-int main(int argc, char** argv) {
-  const int nf = argc > 1 ? std::atoi(argv[1]) : 16;
-  const int reps = argc > 2 ? std::atoi(argv[2]) : 5;
-  const int ns = argc > 3 ? std::atoi(argv[3]) : 8192;
+template <int NC>
+int run(int nf, int reps, int ns, int nrx) {
   const float* map = nullptr;
   Cfar2DArgs a{};
   // the reference core's 2-D CFAR parameters (fmcw_api.hip cfar2_args with the defaults)
@@ -109,14 +110,19 @@ int main(int argc, char** argv) {
   a.compat = 0;
   a.s_min = 2.f;
   std::vector<Var> vars;
-  vars.push_back({"k_cfar2d (production)", reinterpret_cast<const void*>(k_cfar2d<NC, 6, 2, 5, 1>),
-                  cfar2d_smem_bytes<NC>(a.hr), [&](int grid, size_t smem, int n_strips, int steps, DetSink sink) {
+  vars.push_back({"k_cfar2d + decide + emit (production)", reinterpret_cast<const void*>(k_cfar2d<NC, 6, 2, 5, 1>),
+                  cfar2d_smem_bytes<NC>(a.hr), [&](int grid, size_t smem, int n_strips, int steps, DetSink sink,
+                                                   Cfar2Cands cands) {
+                    hipMemsetAsync(cands.ctr, 0, 8, 0);
                     hipLaunchKernelGGL((k_cfar2d<NC, 6, 2, 5, 1>), dim3(grid), dim3(256), smem, 0, map, ns, n_strips,
-                                       steps, 0, 0, a, sink);
+                                       steps, 0, 0, a, sink, cands);
+                    hipLaunchKernelGGL(k_cfar2d_decide<NC>, dim3(1024), dim3(256), 0, 0, map, ns, a, cands);
+                    hipLaunchKernelGGL(k_cfar2d_emit<NC>, dim3(256), dim3(256), 0, 0, map, ns, 0, a, cands, sink);
                   }});
 #ifdef K3_LAB_PREV
   vars.push_back({"k_cfar2d (previous)", reinterpret_cast<const void*>(prev::k_cfar2d<NC, 6, 2>),
-                  prev::cfar2d_smem_bytes<NC>(a.hr), [&](int grid, size_t smem, int n_strips, int steps, DetSink sink) {
+                  prev::cfar2d_smem_bytes<NC>(a.hr), [&](int grid, size_t smem, int n_strips, int steps, DetSink sink,
+                                                         Cfar2Cands) {
                     prev::Cfar2DArgs pa;
                     static_assert(sizeof(pa) == sizeof(a), "same argument layout");
                     std::memcpy(&pa, &a, sizeof(a));
@@ -131,7 +137,7 @@ int main(int argc, char** argv) {
   {
     float* m;
     CK(hipMalloc(&m, cells * 4));
-    hipLaunchKernelGGL(k_fill_map, dim3(8192), dim3(256), 0, 0, m, ns, cells);
+    hipLaunchKernelGGL(k_fill_map, dim3(8192), dim3(256), 0, 0, m, ns, NC, nrx, cells);
     map = m;
   }
   const int WR = DopplerGeom<NC>::WR;
@@ -147,12 +153,17 @@ int main(int argc, char** argv) {
   sink.cap = cap;
   sink.slot_cap = slot_cap;
   sink.ovf_base = (uint32_t)tiles * slot_cap;
+  Cfar2Cands cands{};
+  CK(hipMalloc(&cands.cell, cells * 4));
+  CK(hipMalloc(&cands.thr, cells * 4));
+  CK(hipMalloc(&cands.tiles, (size_t)tiles * 4));
+  CK(hipMalloc(&cands.ctr, 16));
   std::vector<uint32_t> ref_cnt, ref_base;
   std::vector<fmcw_det> ref_sc;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  std::printf("map %d frames x %d x %d\n", nf, ns, NC);
+  std::printf("map %d frames x %d x %d, %d rx\n", nf, ns, NC, nrx);
   for (size_t vi = 0; vi < vars.size(); ++vi) {
     const Var& v = vars[vi];
     const size_t smem = v.smem;
@@ -166,7 +177,7 @@ int main(int argc, char** argv) {
     const int grid = std::min(n_strips, grid_max);
     CK(hipMemset(sink.counter, 0, 16));
     CK(hipMemset(sink.wg_count, 0, tiles * 4));
-    v.launch(grid, smem, n_strips, steps, sink);
+    v.launch(grid, smem, n_strips, steps, sink, cands);
     CK(hipGetLastError());
     CK(hipDeviceSynchronize());
     std::vector<uint32_t> cnt(tiles), base(tiles), ctr(4);
@@ -201,7 +212,7 @@ int main(int argc, char** argv) {
     for (int r = 0; r < reps; ++r) {
       CK(hipMemset(sink.counter, 0, 16));
       CK(hipEventRecord(e0, 0));
-      v.launch(grid, smem, n_strips, steps, sink);
+      v.launch(grid, smem, n_strips, steps, sink, cands);
       CK(hipEventRecord(e1, 0));
       CK(hipEventSynchronize(e1));
       float ms;
@@ -214,4 +225,19 @@ int main(int argc, char** argv) {
     std::fflush(stdout);
   }
   return 0;
+}
+
+int main(int argc, char** argv) {
+  const int nf = argc > 1 ? std::atoi(argv[1]) : 16;
+  const int reps = argc > 2 ? std::atoi(argv[2]) : 5;
+  const int ns = argc > 3 ? std::atoi(argv[3]) : 8192;
+  const int nc = argc > 4 ? std::atoi(argv[4]) : 1024;
+  const int nrx = argc > 5 ? std::atoi(argv[5]) : 1;
+  switch (nc) {
+    case 1024: return run<1024>(nf, reps, ns, nrx);
+    case 512: return run<512>(nf, reps, ns, nrx);
+    case 256: return run<256>(nf, reps, ns, nrx);
+  }
+  std::fprintf(stderr, "nc %d not instantiated\n", nc);
+  return 2;
 }
