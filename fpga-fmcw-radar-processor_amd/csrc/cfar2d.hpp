@@ -473,36 +473,33 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
   uint32_t* const cnt = aux + kCoopRound;
   const int tid = opaque(threadIdx.x);
 
-  // one float4 of cells (row x, Doppler d..d+3) into the ring, with its circular-halo copy: the
-  // key16 of each cell, and 4 bytes of the screen row -- LV: level nibbles; else the pair-max 7-bit
-  // keys (which need the cell d+4 after it, circularly, in v4)
-  // per strip: LV level words (qa2, qb2), else the 7-bit key base kb
+  // The ring rows of one float4 of cells (row x, Doppler d..d+3), each with its circular-halo copy:
+  // put_k16 the key16 row (returns the 4 keys), put_scr 4 bytes of the screen row -- LV: level
+  // nibbles; else the pair-max 7-bit keys (which need the cell d + 4 after it, circularly).
+  // Per strip: LV level words (qa2, qb2), else the 7-bit key base kb.
   uint32_t qa2 = 0u, qb2 = 0u;
   int kb = 0;
-  auto put4 = [&](const RowRing& rr, int x, int d, float4 v, float v4) {
+  auto put_k16 = [&](const RowRing& rr, int x, int d, float4 v) -> uint2 {
     v = a.compat ? q17x4(v) : nonneg4(v);
     const uint2 kw = make_uint2(key16(v.x) | (key16(v.y) << 16), key16(v.z) | (key16(v.w) << 16));
-    uint32_t w;
-    if constexpr (LV) {
-      (void)v4;
-      w = lv_nibbles(kw, qa2, qb2);
-    } else {
-      v4 = a.compat ? q17(v4) : nonneg(v4);
-      const uint32_t k0 = key7(v.x, kb), k1 = key7(v.y, kb), k2 = key7(v.z, kb), k3 = key7(v.w, kb), k4 = key7(v4, kb);
-      w = max(k0, k1) | (max(k1, k2) << 8) | (max(k2, k3) << 16) | (max(k3, k4) << 24) | 0x80808080u;
-    }
-    uint8_t* row = rr.row(x);
     uint16_t* krow = rr.krow(x);
-    *reinterpret_cast<uint32_t*>(row + b7idx(d)) = w;
     *reinterpret_cast<uint2*>(krow + k16idx(d)) = kw;
-    if (d < MH) {
-      *reinterpret_cast<uint32_t*>(row + b7idx(NC + d)) = w;
-      *reinterpret_cast<uint2*>(krow + k16idx(NC + d)) = kw;
-    }
-    if (d >= NC - MH) {
-      *reinterpret_cast<uint32_t*>(row + b7idx(d - NC)) = w;
-      *reinterpret_cast<uint2*>(krow + k16idx(d - NC)) = kw;
-    }
+    if (d < MH) *reinterpret_cast<uint2*>(krow + k16idx(NC + d)) = kw;
+    if (d >= NC - MH) *reinterpret_cast<uint2*>(krow + k16idx(d - NC)) = kw;
+    return kw;
+  };
+  auto put_scr = [&](const RowRing& rr, int x, int d, uint32_t w) {
+    uint8_t* row = rr.row(x);
+    *reinterpret_cast<uint32_t*>(row + b7idx(d)) = w;
+    if (d < MH) *reinterpret_cast<uint32_t*>(row + b7idx(NC + d)) = w;
+    if (d >= NC - MH) *reinterpret_cast<uint32_t*>(row + b7idx(d - NC)) = w;
+  };
+  // 7-bit pair-max keys of cells d..d+3 from the key16 of cells d..d+4 (key7 = key16 >> 3 - kb)
+  auto pm_word = [&](uint2 kw, uint32_t k4) {
+    auto k7 = [&](uint32_t k16) { return (uint32_t)min(max((int)(k16 >> 3) - kb, 0), 127); };
+    const uint32_t k0 = k7(kw.x & 0xffffu), k1 = k7(kw.x >> 16), k2 = k7(kw.y & 0xffffu), k3 = k7(kw.y >> 16),
+                   k5 = k7(k4);
+    return max(k0, k1) | (max(k1, k2) << 8) | (max(k2, k3) << 16) | (max(k3, k5) << 24) | 0x80808080u;
   };
 
   for (int g = blockIdx.x; g < n_strips; g += gridDim.x) {
@@ -514,73 +511,7 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
     RowRing rr{tile, keys, 0, nr, RB, Gm::KRS};
     float4 pre[4];
     float pre4[4];
-    // the strip's levels (LV) or key base, from the first step's CUT rows (TR x NC = 4096 cells):
-    // their mean level (bits >> 19: 16 levels per octave); LV then the FMCW_K3_LV_QA / _QB quantiles
-    // of a 128-level histogram around that mean
-    uint32_t wa2 = 0u, wb2 = 0u;
-    {
-      uint32_t k7[16];
-      uint32_t s = 0;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int e4 = tid + u * NT;
-        const int i = e4 / (NC / 4), d = (e4 - i * (NC / 4)) * 4;
-        const int rs = min(t_beg * TR + i, ns - 1);
-        float4 v = *reinterpret_cast<const float4*>(fm + (size_t)rs * NC + d);
-        v = a.compat ? q17x4(v) : nonneg4(v);
-        k7[4 * u] = min(__float_as_uint(v.x), 0x7f800000u) >> FMCW_K3_KEY_SHIFT;
-        k7[4 * u + 1] = min(__float_as_uint(v.y), 0x7f800000u) >> FMCW_K3_KEY_SHIFT;
-        k7[4 * u + 2] = min(__float_as_uint(v.z), 0x7f800000u) >> FMCW_K3_KEY_SHIFT;
-        k7[4 * u + 3] = min(__float_as_uint(v.w), 0x7f800000u) >> FMCW_K3_KEY_SHIFT;
-        s += k7[4 * u] + k7[4 * u + 1] + k7[4 * u + 2] + k7[4 * u + 3];
-      }
-#pragma unroll
-      for (int x = 32; x >= 1; x >>= 1) s += (uint32_t)__shfl_xor((int)s, x, 64);
-      __syncthreads();  // the previous strip is done with cnt and list
-      if (threadIdx.x == 0) cnt[12] = 0u;
-      if (LV && threadIdx.x < 128) list[threadIdx.x] = 0u;
-      __syncthreads();
-      if (lane == 0) atomicAdd(&cnt[12], s);
-      __syncthreads();
-      const int mean7 = (int)(cnt[12] / (uint32_t)(TR * NC));
-      if constexpr (LV) {
-        const int h0 = mean7 - 64;  // histogram bin 0
-#pragma unroll
-        for (int i = 0; i < 16; ++i) atomicAdd(&list[min(max((int)k7[i] - h0, 0), 127)], 1u);
-        __syncthreads();
-        if (wv == 0) {
-          // bins 2 lane, 2 lane + 1: inclusive counts; the quantile bin = the first reaching p N
-          const uint32_t c0 = list[2 * lane], c1 = list[2 * lane + 1];
-          int tot;
-          const uint32_t ex = (uint32_t)wave_excl_scan((int)(c0 + c1), tot);
-          const uint32_t cum0 = ex + c0, cum1 = ex + c0 + c1;
-          const uint32_t na = (uint32_t)(FMCW_K3_LV_QA * (TR * NC) / 1000), nb = (uint32_t)(FMCW_K3_LV_QB * (TR * NC) / 1000);
-          const uint64_t ba0 = __ballot(cum0 >= na), ba1 = __ballot(cum1 >= na);
-          const uint64_t bb0 = __ballot(cum0 >= nb), bb1 = __ballot(cum1 >= nb);
-          // first bin: lane l's bin 2l if its cum0 qualifies, else 2l + 1
-          auto first_bin = [](uint64_t m0, uint64_t m1) {
-            const int l = __builtin_ctzll(m1);  // cum1 is reached by every qualifying lane
-            return (m0 >> l) & 1u ? 2 * l : 2 * l + 1;
-          };
-          if (lane == 0) {
-            cnt[14] = (uint32_t)first_bin(ba0, ba1);
-            cnt[15] = (uint32_t)first_bin(bb0, bb1);
-          }
-        }
-        __syncthreads();
-        // level keys QA <= QB (key16 units: key7 << 3) and the CUT bounds U = key16(fl(s_min lo(Q))), as
-        // the words lv_nibbles / cfar2d_screen_lv compare against
-        const uint32_t QA = (uint32_t)min(max((h0 + (int)cnt[14]) * 8, 1), 0x7f80);
-        const uint32_t QB = (uint32_t)min(max((h0 + (int)cnt[15]) * 8, 1), 0x7f80);
-        qa2 = QA | (QA << 16);
-        qb2 = QB | (QB << 16);
-        const uint32_t UA = key16(a.s_min * key_lo(QA)), UB = key16(a.s_min * key_lo(QB));
-        wa2 = ((UA | 0x8000u) - 1u) * 0x00010001u;
-        wb2 = ((UB | 0x8000u) - 1u) * 0x00010001u;
-      } else {
-        kb = mean7 - FMCW_K3_KEY_LOW;
-      }
-    }
+    uint32_t wa2 = 0u, wb2 = 0u;  // LV: the CUT bounds of the two levels (cfar2d_screen_lv)
     for (int t = t_beg; t < t_end; ++t) {
       const int wt0 = t * WPB;                             // first wave tile of this step
       const int n_wt = min(WPB, wt_per_frame - wt0);
@@ -591,29 +522,97 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
       const int r = r0 + rlw;
       __syncthreads();  // the previous step's waves are done with the rows and the lists
       if (t == t_beg) {
-        // rows r0-hr .. r0+TR+hr-1 (zero outside the map), 4 float4 loads in flight per lane
+        // rows r0-hr .. r0+TR+hr-1 (zero outside the map), 4 float4 loads in flight per lane: the
+        // key16 rows first, then the strip's levels (or key base) from the staged keys of the first
+        // step's CUT rows, then the screen rows from the keys
         const int n4 = nr * (NC / 4);
         for (int b = tid; b < n4; b += 4 * NT) {
           float4 v[4];
-          float v4[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int e4 = b + u * NT;
             const int x = e4 / (NC / 4), d = (e4 - x * (NC / 4)) * 4;
             const int r = r0 - a.hr + x;
             v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-            v4[u] = 0.f;
-            if (e4 < n4 && r >= 0 && r < ns) {
-              v[u] = *reinterpret_cast<const float4*>(fm + (size_t)r * NC + d);
-              if constexpr (!LV) v4[u] = fm[(size_t)r * NC + ((d + 4) & (NC - 1))];
-            }
+            if (e4 < n4 && r >= 0 && r < ns) v[u] = *reinterpret_cast<const float4*>(fm + (size_t)r * NC + d);
           }
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int e4 = b + u * NT;
             const int x = e4 / (NC / 4), d = (e4 - x * (NC / 4)) * 4;
-            if (e4 < n4) put4(rr, x, d, v[u], v4[u]);
+            if (e4 < n4) put_k16(rr, x, d, v[u]);
           }
+        }
+        if (threadIdx.x == 0) cnt[12] = 0u;
+        if (LV && threadIdx.x < 128) list[threadIdx.x] = 0u;
+        __syncthreads();
+        // the first step's CUT rows (TR x NC = 4096 cells; ring rows hr .. hr + TR - 1): their mean
+        // level key16 >> 3 (= bits >> 19: 16 levels per octave), then (LV) the FMCW_K3_LV_QA / _QB
+        // quantiles of a 128-level histogram around that mean
+        uint32_t k7[16];
+        {
+          uint32_t sum = 0;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int e4 = tid + u * NT;
+            const int i = e4 / (NC / 4), d = (e4 - i * (NC / 4)) * 4;
+            const uint2 kw = *reinterpret_cast<const uint2*>(rr.krow(a.hr + i) + k16idx(d));
+            k7[4 * u] = (kw.x & 0xffffu) >> 3;
+            k7[4 * u + 1] = kw.x >> 19;
+            k7[4 * u + 2] = (kw.y & 0xffffu) >> 3;
+            k7[4 * u + 3] = kw.y >> 19;
+            sum += k7[4 * u] + k7[4 * u + 1] + k7[4 * u + 2] + k7[4 * u + 3];
+          }
+#pragma unroll
+          for (int x = 32; x >= 1; x >>= 1) sum += (uint32_t)__shfl_xor((int)sum, x, 64);
+          if (lane == 0) atomicAdd(&cnt[12], sum);
+        }
+        __syncthreads();
+        const int mean7 = (int)(cnt[12] / (uint32_t)(TR * NC));
+        if constexpr (LV) {
+          const int h0 = mean7 - 64;  // histogram bin 0
+#pragma unroll
+          for (int i = 0; i < 16; ++i) atomicAdd(&list[min(max((int)k7[i] - h0, 0), 127)], 1u);
+          __syncthreads();
+          if (wv == 0) {
+            // bins 2 lane, 2 lane + 1: inclusive counts; the quantile bin = the first reaching p N
+            const uint32_t c0 = list[2 * lane], c1 = list[2 * lane + 1];
+            int tot;
+            const uint32_t ex = (uint32_t)wave_excl_scan((int)(c0 + c1), tot);
+            const uint32_t cum0 = ex + c0, cum1 = ex + c0 + c1;
+            const uint32_t na = (uint32_t)(FMCW_K3_LV_QA * (TR * NC) / 1000), nb = (uint32_t)(FMCW_K3_LV_QB * (TR * NC) / 1000);
+            const uint64_t ba0 = __ballot(cum0 >= na), ba1 = __ballot(cum1 >= na);
+            const uint64_t bb0 = __ballot(cum0 >= nb), bb1 = __ballot(cum1 >= nb);
+            // first bin: lane l's bin 2l if its cum0 qualifies, else 2l + 1
+            auto first_bin = [](uint64_t m0, uint64_t m1) {
+              const int l = __builtin_ctzll(m1);  // cum1 is reached by every qualifying lane
+              return (m0 >> l) & 1u ? 2 * l : 2 * l + 1;
+            };
+            if (lane == 0) {
+              cnt[14] = (uint32_t)first_bin(ba0, ba1);
+              cnt[15] = (uint32_t)first_bin(bb0, bb1);
+            }
+          }
+          __syncthreads();
+          // level keys QA <= QB (key16 units: key7 << 3) and the CUT bounds U = key16(fl(s_min lo(Q))),
+          // as the words lv_nibbles / cfar2d_screen_lv compare against
+          const uint32_t QA = (uint32_t)min(max((h0 + (int)cnt[14]) * 8, 1), 0x7f80);
+          const uint32_t QB = (uint32_t)min(max((h0 + (int)cnt[15]) * 8, 1), 0x7f80);
+          qa2 = QA | (QA << 16);
+          qb2 = QB | (QB << 16);
+          const uint32_t UA = key16(a.s_min * key_lo(QA)), UB = key16(a.s_min * key_lo(QB));
+          wa2 = ((UA | 0x8000u) - 1u) * 0x00010001u;
+          wb2 = ((UB | 0x8000u) - 1u) * 0x00010001u;
+        } else {
+          kb = mean7 - FMCW_K3_KEY_LOW;
+        }
+        // the screen rows of the whole ring from its key16 rows (halos included)
+        for (int e4 = tid; e4 < n4; e4 += NT) {
+          const int x = e4 / (NC / 4), d = (e4 - x * (NC / 4)) * 4;
+          const uint16_t* kr = rr.krow(x) + k16idx(d);
+          const uint2 kw = *reinterpret_cast<const uint2*>(kr);
+          if constexpr (LV) put_scr(rr, x, d, lv_nibbles(kw, qa2, qb2));
+          else put_scr(rr, x, d, pm_word(kw, (uint32_t)kr[4]));
         }
       } else {
         // the ring turns by TR rows; the TR new rows (prefetched during the previous step) go
@@ -624,7 +623,13 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
         for (int u = 0; u < 4; ++u) {
           const int e4 = tid + u * NT;
           const int i = e4 / (NC / 4), d = (e4 - i * (NC / 4)) * 4;
-          put4(rr, nr - TR + i, d, pre[u], pre4[u]);
+          const uint2 kw = put_k16(rr, nr - TR + i, d, pre[u]);
+          if constexpr (LV) {
+            put_scr(rr, nr - TR + i, d, lv_nibbles(kw, qa2, qb2));
+          } else {
+            const float v4 = a.compat ? q17(pre4[u]) : nonneg(pre4[u]);
+            put_scr(rr, nr - TR + i, d, pm_word(kw, key16(v4)));
+          }
         }
       }
       if (t + 1 < t_end) {  // prefetch the next step's new rows r0 + TR + hr .. (zero past the map)
