@@ -1,5 +1,34 @@
+"""NumPy model of K3's phase-A screens on the bench's own maps (round 4): the fraction of cells each
+screen passes to the candidate test, for the round-3 pair screen, mean-offset levels and quantile
+levels (cfar2d.hpp FMCW_K3_LV_QA / _QB), against the exact E(s_min) >= need test.  The maps are the
+bench's synthetic frames (seed 1234) through the C restatement (oracle/fmcw_cpu.c); rows sampled at
+5 positions, 48 CUT rows each.  usage: python tools/k3_screen_model.py"""
+import sys
+from pathlib import Path
+
 import numpy as np
-Z=np.load("/tmp/sim/maps.npz")
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "fpga-fmcw-radar-processor_amd"))
+sys.path.insert(0, str(REPO / "oracle"))
+
+
+def bench_maps():
+    import cpu_backend as CB
+    from fmcw import synth
+    out = {}
+    for name, (ns, nc, nrx, dt) in {"c5": (8192, 1024, 1, "f16"), "c3": (4096, 512, 4, "f32"),
+                                    "c2": (1024, 256, 1, "f32")}.items():
+        cube = synth.frames(1, ns, nc, nrx, "two_targets", seed=1234, dtype=dt)
+        if not np.iscomplexobj(cube):
+            x = cube.astype(np.float32)
+            cube = x[..., 0] + 1j * x[..., 1]
+        m, _, _ = CB.process(cube.astype(np.complex64), None, threads=8)
+        out[name] = m[0]
+    return out
+
+
+Z = bench_maps()
 hr,gr,hd,gd=5,1,6,2
 offs=[(dr,dd) for dr in range(-hr,hr+1) for dd in range(-hd,hd+1) if not (abs(dr)<=gr and abs(dd)<=gd)]
 need=32; s=np.float32(2.0)
