@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out
+OUT=${GPU_RUN_OUT:-gpurun_out}
 mkdir -p "$OUT"
 run() {  # name limit cmd...
   local name=$1 lim=$2; shift 2
@@ -67,6 +67,9 @@ for s in "$@"; do
     pmc3_fetch) run pmc3_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc3_fetch" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
     pmc3_write) run pmc3_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc3_write" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
     pmc3_sq) run pmc3_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_ACTIVE_INST_ANY -d "$OUT/pmc3_sq" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
+    pmc3_sq2) run pmc3_sq2 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_SALU -d "$OUT/pmc3_sq2" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
+    gloo2)  # N = 2 ranks on this one GPU over gloo: a rehearsal of bench.py's launch, barrier and max-over-ranks timing
+      run bench_2rank_gloo 600 env FMCW_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline --no-h2d --no-sub --frames 256 ;;
     k3lab) run k3lab_c5 300 tools/k3_lab 16 5 ;;
     k3labs)  # every tools/k3_lab_<variant> binary (built on the CPU host with other -D switches)
       for b in tools/k3_lab_*; do run "k3lab_c5_${b#tools/k3_lab_}" 300 "$b" 16 5; done ;;

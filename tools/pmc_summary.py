@@ -16,7 +16,7 @@ gfx950 correction: FETCH_SIZE reports half the bytes of a wide coalesced streami
 is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.  Units of both: KiB.
 
 usage: python tools/pmc_summary.py --fetch F.csv --write W.csv [--sq SQ.csv]
-       --frames c2=5120 --frames c3=112 --frames c5=112 --out profiles/pmc_r03.json
+       --frames c2=5120 --frames c3=80 --frames c5=80 --out profiles/pmc_r04.json
 """
 import argparse
 import collections
@@ -26,8 +26,10 @@ import re
 
 PATTERNS = {
     "c2": {"k_range": r"k_range\w*<1024,", "k_doppler": r"k_doppler<256,"},
-    "c3": {"k_range": r"k_range\w*<4096,", "k_doppler": r"k_doppler<512,", "k_cfar": r"k_cfar2d<512,"},
-    "c5": {"k_range": r"k_range(\w*<8192,|_px<)", "k_doppler": r"k_doppler<1024,", "k_cfar": r"k_cfar2d<1024,"},
+    # K3 = the three launches of a 2-D CFAR batch (k_cfar2d, k_cfar2d_decide, k_cfar2d_emit; round 4)
+    "c3": {"k_range": r"k_range\w*<4096,", "k_doppler": r"k_doppler<512,", "k_cfar": r"k_cfar2d(_decide|_emit)?<512[,>]"},
+    "c5": {"k_range": r"k_range(\w*<8192,|_px<)", "k_doppler": r"k_doppler<1024,",
+           "k_cfar": r"k_cfar2d(_decide|_emit)?<1024[,>]"},
 }
 ALG = {  # algorithmic bytes per frame, fp32 spectrum
     "c2": {"k_range": 1024 * 256 * 16, "k_doppler": 1024 * 256 * 12},
@@ -60,7 +62,7 @@ def main():
     ap.add_argument("--sq", default=None)
     ap.add_argument("--frames", action="append", default=[], help="workload=frames processed in the run")
     ap.add_argument("--command", default="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-h2d")
-    ap.add_argument("--out", default="profiles/pmc_r03.json")
+    ap.add_argument("--out", default="profiles/pmc_r04.json")
     a = ap.parse_args()
     frames = {k: int(v) for k, v in (x.split("=") for x in a.frames)}
     tables = [read(a.fetch), read(a.write)] + ([read(a.sq)] if a.sq else [])
@@ -68,21 +70,29 @@ def main():
                      + a.command + "`; per kernel: sum over its launches / frames it processed; "
                      "FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes",
            "frames": frames, "workloads": {}}
+    # several kernel names may map to one (workload, kernel) entry (K3's three launches): the counters
+    # are summed over all of them
+    tot = collections.defaultdict(float)
     for t in tables:
         for name, ctrs in t.items():
             w, k = classify(name)
             if not w or w not in frames:
                 continue
-            ent = out["workloads"].setdefault(w, {"kernels": {}})["kernels"].setdefault(k, {"name": name})
+            ent = out["workloads"].setdefault(w, {"kernels": {}})["kernels"].setdefault(k, {"names": []})
+            if name not in ent["names"]:
+                ent["names"].append(name)
             for c, vals in ctrs.items():
-                tot = sum(vals)
-                if c == "FETCH_SIZE":
-                    ent["fetch_bytes_per_frame"] = tot * 2 * 1024 / frames[w]
-                elif c == "WRITE_SIZE":
-                    ent["write_bytes_per_frame"] = tot * 1024 / frames[w]
-                else:
-                    ent[c + "_per_frame"] = tot / frames[w]
-                ent["launches"] = len(vals)
+                tot[(w, k, c)] += sum(vals)
+                if c in ("FETCH_SIZE", "WRITE_SIZE") and re.search(r"k_cfar2d<|k_range|k_doppler", name):
+                    ent["launches"] = len(vals)
+    for (w, k, c), v in tot.items():
+        ent = out["workloads"][w]["kernels"][k]
+        if c == "FETCH_SIZE":
+            ent["fetch_bytes_per_frame"] = v * 2 * 1024 / frames[w]
+        elif c == "WRITE_SIZE":
+            ent["write_bytes_per_frame"] = v * 1024 / frames[w]
+        else:
+            ent[c + "_per_frame"] = v / frames[w]
     for w, d in out["workloads"].items():
         for k, e in d["kernels"].items():
             if "fetch_bytes_per_frame" in e and "write_bytes_per_frame" in e:
