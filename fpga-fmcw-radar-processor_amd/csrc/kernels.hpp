@@ -1528,7 +1528,9 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
         }
         v[m] = x;
       }
+#ifndef FMCW_K2_ABLATE_FFT  // timing experiments only (round 4): 1 = no FFT arithmetic (data movement kept)
       Dft<16>::run(v);                       // pass 1: L = 1, no twiddles
+#endif
       {
         float2* d = buf + pad16(16 * t);     // y[16 t + m]
 #pragma unroll
@@ -1541,6 +1543,12 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
         prefetch(same ? tile : tile + tile_step, same ? rx + 1 : 0);
       }
       float2 X[LG][LR];
+#ifdef FMCW_K2_ABLATE_FFT
+      if constexpr (TWH) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) X[0][m] = buf[pad16(t) + padoff(m * 16)];
+      } else
+#endif
       if constexpr (TWH) stockham_last_tw<NC, 16, P>(buf, t, X, twh);
       else stockham_to_regs<NC, 16, P, false>(buf, t, X);
       if (!FAST && mag_mode == FMCW_MAG_AMBM) {  // uniform: one branch for the whole block
