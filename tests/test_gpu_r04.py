@@ -17,7 +17,7 @@ import cpu_backend as CB
 import fmcw_oracle as O
 from conftest import REPO
 from fmcw import RadarCore, synth
-from test_gpu_parity import check_map, to_complex
+from test_gpu_parity import check_map, run_cfar_stage, to_complex
 
 pytestmark = pytest.mark.gpu
 
@@ -47,3 +47,51 @@ def test_bench_shape_parity(wl):
     assert set(out.dets["frame"].tolist()) == set(range(F))
     hit = set(zip(out.dets["frame"].tolist(), out.dets["range"].tolist(), out.dets["doppler"].tolist()))
     assert (0, round(100 * ns / 1024), 5) in hit and (F - 1, round(100 * ns / 1024), 5) in hit
+
+
+@pytest.mark.parametrize("want_map,map_kind", [(False, "linear"), (True, "db")])
+def test_cfar2d_on_chunk_scratch(want_map, map_kind):
+    """No linear map from the caller (map-less call, or a dB map): the 2-D CFAR runs per K1/K2
+    chunk on the handle's scratch map, one K3 launch (and candidate-counter slot) per chunk --
+    7 chunks of 3 frames here.  Detections bit-exact vs the C oracle on the linear map of the
+    same frames (from a linear-map handle, itself checked against the oracle elsewhere)."""
+    ns, nc, nf = 1024, 256, 20
+    cube = synth.frames(nf, ns, nc, 1, "random_target", seed=41)
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os2d", max_frames=nf, chunk_frames=3) as core:
+        lin = core.process(cube).rd_map
+    want = CB.cfar(lin, O.Cfar2D(), threads=16)
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os2d", max_frames=nf, chunk_frames=3,
+                   map_kind=map_kind) as core:
+        out = core.process(cube, want_map=want_map)
+    np.testing.assert_array_equal(out.dets, want)
+    assert out.n_dets >= nf
+
+
+def test_cfar2d_stage_in_pieces():
+    """fmcw_cfar on more frames than one K3 launch's candidate list holds (16 + chunk): the stage
+    runs in pieces, each with its own counters; the list is the oracle's, in order."""
+    ns, nc, nf = 256, 128, 45
+    rng = np.random.default_rng(43)
+    m = rng.rayleigh(10.0, (nf, ns, nc)).astype(np.float32)
+    m[:, 60, 17] = 800.0
+    m[::3, 150:153, 90] = 400.0
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os2d", max_frames=nf, chunk_frames=2) as core:
+        got = run_cfar_stage(core, m, cap=1 << 18)
+    want = CB.cfar(m, O.Cfar2D(), threads=16)
+    np.testing.assert_array_equal(got, want)
+    assert set(got["frame"].tolist()) == set(range(nf))
+
+
+def test_cfar2d_dense_candidates_exact_count():
+    """A lattice where ~1/9 of all cells detect (every candidate run is long, many tiles spill into
+    the overflow region): the candidate list (room for every cell) keeps the count exact, and the
+    records equal the oracle's."""
+    ns, nc, nf = 512, 256, 2
+    rng = np.random.default_rng(47)
+    m = rng.rayleigh(1.0, (nf, ns, nc)).astype(np.float32)
+    m[:, ::3, ::3] = 50.0
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os2d", max_frames=nf) as core:
+        got = run_cfar_stage(core, m, cap=1 << 20)
+    want = CB.cfar(m, O.Cfar2D(), threads=16)
+    assert len(want) > nf * ns * nc // 12
+    np.testing.assert_array_equal(got, want)
