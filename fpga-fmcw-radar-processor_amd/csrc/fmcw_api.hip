@@ -5,6 +5,7 @@
 // configuration once, uploads the window tables (window_multiplier.vhd:34-49, as fp32) and
 // allocates every scratch buffer, so fmcw_enqueue only launches kernels (graph-capturable).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cmath>
@@ -377,27 +378,40 @@ hipEvent_t take_event(fmcw_handle* h) {
   return e;
 }
 
+// Per-kernel timing (fmcw_set_profiling): the scope's first launch takes the start event and its
+// last launch the stop event through hipExtLaunchKernelGGL, so the events carry the dispatches'
+// own begin / end timestamps -- the kernels' span, as rocprofv3's kernel trace reports it, without
+// the event marker packets (and their dispatch gaps) that hipEventRecord around a launch adds.
 struct ProfScope {
   fmcw_handle* h;
   int kid;
-  hipStream_t s;
-  hipEvent_t a = nullptr;
-  ProfScope(fmcw_handle* h_, int kid_, hipStream_t s_) : h(h_), kid(kid_), s(s_) {
+  hipEvent_t a = nullptr, b = nullptr;
+  bool started = false;
+  ProfScope(fmcw_handle* h_, int kid_) : h(h_), kid(kid_) {
     if (h->profiling) {
       a = take_event(h);
-      if (a) hipEventRecord(a, s);
+      b = a ? take_event(h) : nullptr;
+      if (!b && a) h->free_events.push_back(a), a = nullptr;
     }
   }
+  // events for one launch of the scope: start on the first, stop on the one flagged last
+  hipEvent_t start() {
+    if (started) return nullptr;
+    started = true;
+    return a;
+  }
+  hipEvent_t stop(bool last) const { return last ? b : nullptr; }
   ~ProfScope() {
-    if (h->profiling && a) {
-      hipEvent_t b = take_event(h);
-      if (b) {
-        hipEventRecord(b, s);
-        h->pending.push_back({kid, a, b});
-      }
-    }
+    if (a && b && started) h->pending.push_back({kid, a, b});
+    else if (a && b) h->free_events.push_back(a), h->free_events.push_back(b);
   }
 };
+// hipLaunchKernelGGL with the scope's events (none outside profiling)
+template <typename F, typename... Args>
+void launch_k(ProfScope& ps, bool last, F fn, dim3 grid, dim3 block, uint32_t smem, hipStream_t s, Args... args) {
+  if (ps.a) hipExtLaunchKernelGGL(fn, grid, block, smem, s, ps.start(), ps.stop(last), 0u, args...);
+  else hipLaunchKernelGGL(fn, grid, block, smem, s, args...);
+}
 
 int check_launch(const char* what) {
   hipError_t e = hipGetLastError();
@@ -470,14 +484,14 @@ int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipS
       const int n_strips = np * ((tpf + steps - 1) / steps);
       const int grid = std::min(n_strips, h->grid_cfar);
       h->cfar2_steps_last = steps;
-      ProfScope ps(h, FMCW_K_CFAR2D, s);
-      hipLaunchKernelGGL(ci.fn, dim3(grid), dim3(256), h->cfar2d_smem, s, mp, (int)c.n_range, n_strips, steps,
-                         frame0 + p0, tile0 + (int)(p0 * tiles_per_frame(h)), a, sink, cands);
+      ProfScope ps(h, FMCW_K_CFAR2D);
+      launch_k(ps, false, ci.fn, dim3(grid), dim3(256), (uint32_t)h->cfar2d_smem, s, mp, (int)c.n_range, n_strips,
+               steps, frame0 + p0, tile0 + (int)(p0 * tiles_per_frame(h)), a, sink, cands);
       if (int rc = check_launch("k_cfar2d")) return rc;
       // K3b / K3c: fixed grids that read the candidate counts on the device (no host round trip)
-      hipLaunchKernelGGL(ci.decide, dim3(kCfar2DecideGrid), dim3(256), 0, s, mp, (int)c.n_range, a, cands);
-      hipLaunchKernelGGL(ci.emit, dim3(kCfar2EmitGrid), dim3(256), 0, s, mp, (int)c.n_range, frame0 + p0, a, cands,
-                         sink);
+      launch_k(ps, false, ci.decide, dim3(kCfar2DecideGrid), dim3(256), 0u, s, mp, (int)c.n_range, a, cands);
+      launch_k(ps, true, ci.emit, dim3(kCfar2EmitGrid), dim3(256), 0u, s, mp, (int)c.n_range, frame0 + p0, a, cands,
+               sink);
       if (int rc = check_launch("k_cfar2d_decide / _emit")) return rc;
     }
     return FMCW_OK;
@@ -487,9 +501,9 @@ int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipS
   const int n_tiles = nf * (int)(c.n_range / di.WR);
   const int wpb = di.NT / 64;  // DopplerGeom<NC>::WPB: wave tiles per workgroup
   const int grid = std::min((n_tiles + wpb - 1) / wpb, h->grid_doppler);
-  ProfScope ps(h, FMCW_K_CFAR2D, s);
-  hipLaunchKernelGGL(cfar1_fn(c.n_doppler), dim3(grid), dim3(di.NT), 0, s, map_chunk, (int)c.n_range,
-                     n_tiles, frame0, tile0, cfar1_args(c), sink);
+  ProfScope ps(h, FMCW_K_CFAR2D);
+  launch_k(ps, true, cfar1_fn(c.n_doppler), dim3(grid), dim3(di.NT), 0u, s, map_chunk, (int)c.n_range, n_tiles,
+           frame0, tile0, cfar1_args(c), sink);
   return check_launch("k_cfar1d");
 }
 
@@ -497,17 +511,20 @@ int launch_det_finish(fmcw_handle* h, size_t n_frames, fmcw_det* dets, size_t de
                       uint32_t* n_dets_dev, hipStream_t s) {
   const int n = (int)(n_frames * tiles_per_frame(h));
   const int nb = (n + 1023) / 1024;
-  ProfScope ps(h, FMCW_K_COMPACT, s);
-  hipLaunchKernelGGL(k_det_scan_blocks, dim3(nb), dim3(1024), 0, s, h->wg_count, h->wg_off, n, h->block_sum);
-  hipLaunchKernelGGL(k_det_scan_top, dim3(1), dim3(1024), 0, s, h->block_sum, nb, n_dets_dev,
-                     (const uint32_t*)(h->counter + 1));
+  ProfScope ps(h, FMCW_K_COMPACT);
+  const bool copy = dets && det_cap;
+  launch_k(ps, false, k_det_scan_blocks, dim3(nb), dim3(1024), 0u, s, (const uint32_t*)h->wg_count, h->wg_off, n,
+           h->block_sum);
+  launch_k(ps, !copy, k_det_scan_top, dim3(1), dim3(1024), 0u, s, h->block_sum, nb, n_dets_dev,
+           (const uint32_t*)(h->counter + 1));
   int rc = check_launch("k_det_scan");
   if (rc) return rc;
-  if (dets && det_cap) {
+  if (copy) {
     // entries past the handle's scratch capacity are never stored: clip to it as well
     const uint32_t cap = (uint32_t)std::min<size_t>(det_cap, h->det_scratch_cap);
-    hipLaunchKernelGGL(k_det_copy, dim3((n + 255) / 256), dim3(256), 0, s, h->det_scratch,
-                       h->det_scratch_cap, h->wg_base, h->wg_count, h->wg_off, h->block_sum, n, dets, cap);
+    launch_k(ps, true, k_det_copy, dim3((n + 255) / 256), dim3(256), 0u, s, (const fmcw_det*)h->det_scratch,
+             h->det_scratch_cap, (const uint32_t*)h->wg_base, (const uint32_t*)h->wg_count,
+             (const uint32_t*)h->wg_off, (const uint32_t*)h->block_sum, n, dets, cap);
     rc = check_launch("k_det_copy");
   }
   return rc;
@@ -803,12 +820,12 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
     const void* src = static_cast<const char*>(cube) + f0 * in_frame_bytes;
     {
       const int n_groups = nf * (int)c.n_rx * (int)(c.n_doppler / ri.T);
-      ProfScope ps(h, FMCW_K_RANGE, s);
+      ProfScope ps(h, FMCW_K_RANGE);
       // MTI off, fp32 window: K1 applies the Doppler window too (FFT linearity; K2 then skips
       // it); with MTI or the RTL-compat integer window K2 applies it after the canceller
       const float* chirp_w = c.mti_mode == FMCW_MTI_OFF && !q15 ? h->win_d : nullptr;
-      hipLaunchKernelGGL(ri.fn, dim3(std::min(n_groups, h->grid_range)), dim3(ri.NT), 0, s, src, h->inter,
-                         h->win_r, chirp_w, (int)c.n_doppler, n_groups, q15_scale(c), status);
+      launch_k(ps, true, ri.fn, dim3(std::min(n_groups, h->grid_range)), dim3(ri.NT), 0u, s, src, h->inter,
+               (const float*)h->win_r, chirp_w, (int)c.n_doppler, n_groups, q15_scale(c), status);
       if ((rc = check_launch("k_range"))) return rc;
     }
     float* lin = nullptr;
@@ -820,11 +837,10 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
       const int n_tiles = nf * (int)(c.n_range / di.WR);
       const int wpb = di.NT / 64;  // DopplerGeom<NC>::WPB
       const int grid = std::min((n_tiles + wpb - 1) / wpb, h->grid_doppler);
-      ProfScope ps(h, FMCW_K_DOPPLER, s);
-      hipLaunchKernelGGL(di.fn, dim3(grid), dim3(di.NT), 0, s, h->inter, h->win_d, (int)c.n_range,
-                         (int)c.n_rx, h->lgT, h->lgRB, n_tiles, (int)f0, (int)(f0 * (c.n_range / di.WR)), lin,
-                         db, c.mag_mode, (c.compat_rtl & FMCW_COMPAT_MTI) ? 1 : 0, q15 ? 1 : 0, cf1,
-                         make_sink(h), status);
+      ProfScope ps(h, FMCW_K_DOPPLER);
+      launch_k(ps, true, di.fn, dim3(grid), dim3(di.NT), 0u, s, (const float2*)h->inter, (const float*)h->win_d,
+               (int)c.n_range, (int)c.n_rx, h->lgT, h->lgRB, n_tiles, (int)f0, (int)(f0 * (c.n_range / di.WR)), lin,
+               db, c.mag_mode, (c.compat_rtl & FMCW_COMPAT_MTI) ? 1 : 0, q15 ? 1 : 0, cf1, make_sink(h), status);
       if ((rc = check_launch("k_doppler"))) return rc;
     }
     if (c.cfar_kind == FMCW_CFAR_OS2D) {
@@ -907,10 +923,11 @@ int fmcw_range_ct(fmcw_handle* h, const void* cube, size_t n_frames, void* spec,
     const int nf = (int)std::min<size_t>(rc_chunk, n_frames - f0);
     const int n_groups = nf * (int)c.n_rx * (int)(c.n_doppler / ri.T);
     {
-      ProfScope ps(h, FMCW_K_RANGE, s);
-      hipLaunchKernelGGL(ri.fn, dim3(std::min(n_groups, h->grid_range)), dim3(ri.NT), 0, s,
-                         static_cast<const char*>(cube) + f0 * in_frame_bytes, h->inter, h->win_r,
-                         (const float*)nullptr, (int)c.n_doppler, n_groups, q15_scale(c), (uint32_t*)nullptr);
+      ProfScope ps(h, FMCW_K_RANGE);
+      launch_k(ps, true, ri.fn, dim3(std::min(n_groups, h->grid_range)), dim3(ri.NT), 0u, s,
+               static_cast<const void*>(static_cast<const char*>(cube) + f0 * in_frame_bytes), h->inter,
+               (const float*)h->win_r, (const float*)nullptr, (int)c.n_doppler, n_groups, q15_scale(c),
+               (uint32_t*)nullptr);
       int rc = check_launch("k_range");
       if (rc) return rc;
     }

@@ -490,13 +490,20 @@ __device__ __forceinline__ void swap32(float2& a, float2& b) {
 // (Measured and dropped: an XOR-swizzled unpadded layout in which pass A stores into exactly the
 // slots its own lane read in the previous pass C, so the barrier between them goes (3 per chirp):
 // 64.9 vs 59.3 us per 3-frame launch, equal at 12 frames -- profiles/r03/k1px/k1lab_c5_sw.log.)
-template <typename LD, int W = 4>
+// WS: range-window values per thread kept in LDS instead of VGPRs (the last WS of the 16).  At 128
+// VGPRs (4 waves per SIMD) the kernel otherwise spills a window value to scratch, and its reload --
+// a vector-memory op issued after the group's 16 tile stores -- makes the next group's pass A wait,
+// in vmcnt order, for every one of those stores.  68 + 2 WS KiB of LDS per workgroup: two still fit
+// a CU (160 KiB) up to WS = 6.
+template <typename LD, int W = 4, int WS = 4>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(W)))
 k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const float* __restrict__ win,
            const float* __restrict__ chirp_w, int nc, int n_groups, float /* q15_scale */, uint32_t* /* status */) {
   constexpr int N = 8192, T = 2, RB = 64;
   static_assert(RangeGeom<N>::T == T && RangeGeom<N>::RB == RB, "tile format of K2");
+  static_assert(WS >= 0 && WS <= 6, "two workgroups per CU");
   __shared__ __attribute__((aligned(16))) float2 lds[padded(N)];
+  __shared__ float wlds[WS > 0 ? WS * 512 : 1];
   const int t0 = threadIdx.x;
   const int lane = t0 & 63, wv = t0 >> 6, h = lane >> 5;
   const int ncb = nc / T;
@@ -517,6 +524,12 @@ k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const floa
     const int vo = opaque(t0) * SB;
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
+#if defined(FMCW_K1_ABLATE) && FMCW_K1_ABLATE == 2  // timing experiments (tools/k1_lab): no cube loads
+      if constexpr (SB == 4) {
+        a[m] = __builtin_bit_cast(Raw1, (uint32_t)(vo * 0x9e3779b1u + m + (uint32_t)chirp));
+        continue;
+      }
+#endif
       if constexpr (SB == 4) {
         a[m] = __builtin_bit_cast(Raw1, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, m * 512 * SB, NTL));
       } else {
@@ -525,11 +538,13 @@ k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const floa
     }
     if (chirp_w) cwn = chirp_w[__builtin_amdgcn_readfirstlane(cb * T + q)];
   };
-  float wh[16];  // range window of samples t + 512 m, held
+  float wh[16 - WS];  // range window of samples t + 512 m, held (m < 16 - WS; the rest in wlds)
 #pragma unroll
-  for (int m = 0; m < 16; ++m) wh[m] = win[t0 + 512 * m];
+  for (int m = 0; m < 16 - WS; ++m) wh[m] = win[t0 + 512 * m];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) asm volatile("" ::"v"(wh[i]));  // complete before the loop (vmcnt order)
+  for (int m = 16 - WS; m < 16; ++m) wlds[(m - 16 + WS) * 512 + t0] = win[t0 + 512 * m];
+#pragma unroll
+  for (int i = 0; i < 16 - WS; ++i) asm volatile("" ::"v"(wh[i]));  // complete before the loop (vmcnt order)
 
   // pass C's group j = kc + 256 h; the pass-D twiddle base W_8192^(kc + 2048 (1 - h))
   const int kc = (lane & 31) + 32 * wv;
@@ -549,7 +564,10 @@ k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const floa
       {  // pass A: window, radix 16 over x[t + 512 m]
         float2 v[16];
 #pragma unroll
-        for (int m = 0; m < 16; ++m) v[m] = LD::expand1_scaled(a[m], wh[m] * cw);
+        for (int m = 0; m < 16; ++m) {
+          const float w = m < 16 - WS ? wh[m < 16 - WS ? m : 0] : wlds[(m - 16 + WS) * 512 + t];
+          v[m] = LD::expand1_scaled(a[m], w * cw);
+        }
         Dft<16>::run(v);
         float2* d = lds + pad16(16 * t);
 #pragma unroll
@@ -558,6 +576,9 @@ k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const floa
       // the next chirp's input: this group's second chirp, or the next group's first
       if (q == 0) fetch(g, 1);
       else if (g + (int)gridDim.x < n_groups) fetch(g + gridDim.x, 0);
+#if defined(FMCW_K1_ABLATE) && FMCW_K1_ABLATE == 3  // timing experiments: no pass B (wrong results)
+      if (false)
+#endif
       {  // pass B: radix 16, L = 16 (in place, barriers around the exchange)
         __syncthreads();
         float2 v[16];
@@ -618,6 +639,9 @@ k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const floa
         const int r = s ? m : m + 8;
         typedef float f4v __attribute__((ext_vector_type(4)));
         const f4v x = {X[0][r].x, X[0][r].y, X[1][r].x, X[1][r].y};
+#if defined(FMCW_K1_ABLATE) && FMCW_K1_ABLATE == 1  // timing experiments: no spectrum stores
+        if (x.x != 1234.5f) continue;
+#endif
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(fmcw_u4v, x), rs, vo, (4 * m + 64 * s) * ncb * 1024,
                                                FMCW_K1_PX_POLICY);
       }
