@@ -119,15 +119,21 @@ int run(int nf, int reps, int ns, int nrx) {
                     hipLaunchKernelGGL(k_cfar2d_decide<NC>, dim3(1024), dim3(256), 0, 0, map, ns, a, cands);
                     hipLaunchKernelGGL(k_cfar2d_emit<NC>, dim3(256), dim3(256), 0, 0, map, ns, 0, a, cands, sink);
                   }});
-#ifdef K3_LAB_PREV
-  vars.push_back({"k_cfar2d (previous)", reinterpret_cast<const void*>(prev::k_cfar2d<NC, 6, 2>),
+#ifdef K3_LAB_PREV  // the previous three-launch K3 (same arguments, its own types)
+  vars.push_back({"k_cfar2d + decide + emit (previous)", reinterpret_cast<const void*>(prev::k_cfar2d<NC, 6, 2, 5, 1>),
                   prev::cfar2d_smem_bytes<NC>(a.hr), [&](int grid, size_t smem, int n_strips, int steps, DetSink sink,
-                                                         Cfar2Cands) {
+                                                         Cfar2Cands cands) {
                     prev::Cfar2DArgs pa;
                     static_assert(sizeof(pa) == sizeof(a), "same argument layout");
                     std::memcpy(&pa, &a, sizeof(a));
-                    hipLaunchKernelGGL((prev::k_cfar2d<NC, 6, 2>), dim3(grid), dim3(256), smem, 0, map, ns,
-                                       n_strips, steps, 0, 0, pa, sink);
+                    prev::Cfar2Cands pc;
+                    static_assert(sizeof(pc) == sizeof(cands), "same candidate-list layout");
+                    std::memcpy(&pc, &cands, sizeof(cands));
+                    hipMemsetAsync(cands.ctr, 0, 8, 0);
+                    hipLaunchKernelGGL((prev::k_cfar2d<NC, 6, 2, 5, 1>), dim3(grid), dim3(256), smem, 0, map, ns,
+                                       n_strips, steps, 0, 0, pa, sink, pc);
+                    hipLaunchKernelGGL(prev::k_cfar2d_decide<NC>, dim3(1024), dim3(256), 0, 0, map, ns, pa, pc);
+                    hipLaunchKernelGGL(prev::k_cfar2d_emit<NC>, dim3(256), dim3(256), 0, 0, map, ns, 0, pa, pc, sink);
                   }});
 #endif
   hipDeviceProp_t prop;
