@@ -230,4 +230,3 @@ def test_cfar1d_screen_is_exact(seed, rank):
     assert det_sort[10, 40]
     if rank == 12:
         assert surv.mean() < 0.05      # the screen clears almost every noise cell
-
