@@ -67,8 +67,6 @@ def parse():
     ap.add_argument("--gather", default="rccl", choices=["rccl", "torch"],
                     help="N > 1: libfmcw's RCCL gather-to-root (no host sync) or torch all_gather")
     ap.add_argument("--no-h2d", action="store_true", help="skip the H2D-inclusive measurement")
-    ap.add_argument("--graphs", type=int, default=1, choices=[0, 1],
-                    help="libfmcw FMCW_PARAM_GRAPHS: 1 = repeated steps replay a captured hipGraph (default)")
     ap.add_argument("--spectrum", default="f32", choices=["f32", "f16"],
                     help="element type of the corner-turned spectrum (fmcw.h fmcw_spectrum_dtype)")
     return ap.parse_args()
@@ -150,7 +148,6 @@ def run_workload(name, args, world, rank, dev, primary, pmc, n_cu):
     core = RadarCore(N_RANGE=ns, N_DOPPLER=nc, N_RX=nrx, in_dtype=wl["dtype"], cfar=wl["cfar"],
                      max_frames=F, chunk_frames=args.chunk if primary else 0, device=local,
                      spectrum=args.spectrum if primary else "f32")
-    core.set_param("graphs", args.graphs)
     # synthetic input: 16 distinct frames (seed 1234 + global frame), tiled to F, resident in HBM
     n_u = min(16, F)
     first_global = rank * F
@@ -275,7 +272,6 @@ def run_workload(name, args, world, rank, dev, primary, pmc, n_cu):
                    "n_samples": ns, "n_rx": nrx, "cfar": wl["cfar"], "rd_map": "linear fp32, written",
                    "spectrum": spectrum,
                    "detection_gather": gather_kind if gather else "none",
-                   "launch": "hipGraph replay of the step (FMCW_PARAM_GRAPHS)" if args.graphs else "direct",
                    "parallelism": f"frame-sharded x{world}"},
         "range_kernel": core.info("range_kernel"),
         "chunk_frames": core.info("chunk"),

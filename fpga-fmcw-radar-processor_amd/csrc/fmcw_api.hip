@@ -166,27 +166,6 @@ struct PendingEvent {
   hipEvent_t a, b;
 };
 
-// fmcw_enqueue graph cache (FMCW_PARAM_GRAPHS): one captured launch sequence per argument set
-struct GraphKey {
-  const void* cube;
-  size_t n_frames;
-  const float* rd_map;
-  const fmcw_det* dets;
-  size_t det_cap;
-  const uint32_t* n_dets_dev;
-  bool operator==(const GraphKey& o) const {
-    return cube == o.cube && n_frames == o.n_frames && rd_map == o.rd_map && dets == o.dets && det_cap == o.det_cap &&
-           n_dets_dev == o.n_dets_dev;
-  }
-};
-struct GraphEntry {
-  GraphKey key;
-  hipGraphExec_t exec = nullptr;  // null: seen once, run directly
-  int k3_launch_idx = 0, cfar2_steps_last = 0;  // host-side state the captured call left behind
-  uint64_t last_use = 0;
-};
-constexpr size_t kGraphCacheMax = 8;
-
 }  // namespace
 
 struct fmcw_handle {
@@ -236,11 +215,6 @@ struct fmcw_handle {
   int k3_frames = 0, k3_launches = 0;
   int k3_launch_idx = 0;                // launches of the current call so far
   uint32_t last_status[2] = {0, 0};     // fmcw_process: status words 2, 3 of its last call
-  // graph cache (FMCW_PARAM_GRAPHS): a repeated fmcw_enqueue argument set replays a captured graph
-  int graphs = 1;
-  hipStream_t cap_stream = nullptr;     // capture stream (the caller's may be the legacy default stream)
-  std::vector<GraphEntry> gcache;
-  uint64_t gclock = 0, graph_replays = 0;
   // profiling
   bool profiling = false;
   std::vector<PendingEvent> pending;
@@ -790,8 +764,6 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   return FMCW_OK;
 }
 
-void graph_cache_clear(fmcw_handle* h);
-
 int fmcw_destroy(fmcw_handle* h) {
   if (!h) return FMCW_OK;
   hipSetDevice(h->cfg.device_id);
@@ -806,18 +778,20 @@ int fmcw_destroy(fmcw_handle* h) {
     hipEventDestroy(pe.b);
   }
   for (auto e : h->free_events) hipEventDestroy(e);
-  graph_cache_clear(h);
-  if (h->cap_stream) hipStreamDestroy(h->cap_stream);
   delete h;
   return FMCW_OK;
 }
 
-namespace {
-
-// The launch sequence of one fmcw_enqueue call on stream s (arguments already validated).
-int enqueue_impl(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_map, fmcw_det* dets, size_t det_cap,
-                 uint32_t* n_dets_dev, hipStream_t s) {
+int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_map, fmcw_det* dets,
+                 size_t det_cap, uint32_t* n_dets_dev, void* stream) {
+  if (!h || !cube) return fail(FMCW_EINVAL, "null handle or cube");
   const fmcw_config& c = h->cfg;
+  if (n_frames < 1 || n_frames > c.max_frames)
+    return fail(FMCW_EINVAL, "n_frames=%zu outside [1, max_frames=%u]", n_frames, c.max_frames);
+  if (c.cfar_kind != FMCW_CFAR_NONE && !n_dets_dev)
+    return fail(FMCW_EINVAL, "n_dets_dev is required when a CFAR is configured");
+  HIP_TRY(hipSetDevice(c.device_id));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, c.spectrum_dtype == FMCW_SPEC_F16, h->k1_want);
   const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype == FMCW_SPEC_F16, h->k2_fast);
   const size_t frame_px = (size_t)c.n_range * c.n_doppler;
@@ -882,83 +856,6 @@ int enqueue_impl(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
     }
   }
   if (c.cfar_kind != FMCW_CFAR_NONE) return launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, s);
-  return FMCW_OK;
-}
-
-// Capture enqueue_impl's launches into a graph (on the handle's capture stream: nothing runs).
-int capture_enqueue(fmcw_handle* h, const GraphKey& k, hipGraphExec_t* exec) {
-  if (!h->cap_stream) HIP_TRY(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
-  HIP_TRY(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
-  const int rc = enqueue_impl(h, k.cube, k.n_frames, const_cast<float*>(k.rd_map), const_cast<fmcw_det*>(k.dets),
-                              k.det_cap, const_cast<uint32_t*>(k.n_dets_dev), h->cap_stream);
-  hipGraph_t g = nullptr;
-  const hipError_t e = hipStreamEndCapture(h->cap_stream, &g);
-  if (rc || e != hipSuccess) {
-    if (g) hipGraphDestroy(g);
-    (void)hipGetLastError();
-    return rc ? rc : fail(FMCW_EHIP, "graph capture: %s", hipGetErrorString(e));
-  }
-  const hipError_t ei = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
-  hipGraphDestroy(g);
-  if (ei != hipSuccess) return fail(FMCW_EHIP, "graph instantiate: %s", hipGetErrorString(ei));
-  return FMCW_OK;
-}
-
-}  // namespace
-
-void graph_cache_clear(fmcw_handle* h) {
-  for (auto& e : h->gcache)
-    if (e.exec) hipGraphExecDestroy(e.exec);
-  h->gcache.clear();
-}
-
-// fmcw_enqueue: with FMCW_PARAM_GRAPHS (default on), an argument set seen before is captured once
-// into a hipGraph and replayed from then on -- the same kernels with the same arguments, launched
-// as one graph (a repeated batch loop pays the per-kernel host launch cost once).  The first
-// sighting of an argument set, profiling, a stream the caller is capturing, and
-// FMCW_PARAM_GRAPHS 0 launch directly.
-int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_map, fmcw_det* dets,
-                 size_t det_cap, uint32_t* n_dets_dev, void* stream) {
-  if (!h || !cube) return fail(FMCW_EINVAL, "null handle or cube");
-  const fmcw_config& c = h->cfg;
-  if (n_frames < 1 || n_frames > c.max_frames)
-    return fail(FMCW_EINVAL, "n_frames=%zu outside [1, max_frames=%u]", n_frames, c.max_frames);
-  if (c.cfar_kind != FMCW_CFAR_NONE && !n_dets_dev)
-    return fail(FMCW_EINVAL, "n_dets_dev is required when a CFAR is configured");
-  HIP_TRY(hipSetDevice(c.device_id));
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  if (h->graphs && !h->profiling) HIP_TRY(hipStreamIsCapturing(s, &cap));
-  // the caller's own capture records the launches themselves
-  if (!h->graphs || h->profiling || cap != hipStreamCaptureStatusNone)
-    return enqueue_impl(h, cube, n_frames, rd_map, dets, det_cap, n_dets_dev, s);
-  const GraphKey k{cube, n_frames, rd_map, dets, det_cap, n_dets_dev};
-  GraphEntry* e = nullptr;
-  for (auto& g : h->gcache)
-    if (g.key == k) e = &g;
-  if (!e) {  // first sighting: run directly, remember the arguments (evicting the least recent)
-    if (h->gcache.size() >= kGraphCacheMax) {
-      auto lru = std::min_element(h->gcache.begin(), h->gcache.end(),
-                                  [](const GraphEntry& a, const GraphEntry& b) { return a.last_use < b.last_use; });
-      if (lru->exec) hipGraphExecDestroy(lru->exec);
-      h->gcache.erase(lru);
-    }
-    GraphEntry ne;
-    ne.key = k;
-    ne.last_use = ++h->gclock;
-    h->gcache.push_back(ne);
-    return enqueue_impl(h, cube, n_frames, rd_map, dets, det_cap, n_dets_dev, s);
-  }
-  e->last_use = ++h->gclock;
-  if (!e->exec) {
-    if (int rc = capture_enqueue(h, k, &e->exec)) return rc;
-    e->k3_launch_idx = h->k3_launch_idx;
-    e->cfar2_steps_last = h->cfar2_steps_last;
-  }
-  HIP_TRY(hipGraphLaunch(e->exec, s));
-  h->k3_launch_idx = e->k3_launch_idx;
-  h->cfar2_steps_last = e->cfar2_steps_last;
-  ++h->graph_replays;
   return FMCW_OK;
 }
 
@@ -1083,12 +980,6 @@ int fmcw_set_param(fmcw_handle* h, int key, int64_t value) {
     case FMCW_PARAM_CFAR2D_STEPS:
       if (value < 0 || value > (1 << 20)) return fail(FMCW_EINVAL, "cfar2d steps %lld (0 = cost model)", (long long)value);
       h->cfar2_steps = (int)value;
-      graph_cache_clear(h);  // captured launches carry the old strip length
-      return FMCW_OK;
-    case FMCW_PARAM_GRAPHS:
-      if (value != 0 && value != 1) return fail(FMCW_EINVAL, "graphs %lld (0 or 1)", (long long)value);
-      h->graphs = (int)value;
-      graph_cache_clear(h);
       return FMCW_OK;
   }
   return fail(FMCW_EINVAL, "fmcw_set_param: unknown key %d", key);
@@ -1102,7 +993,6 @@ int fmcw_get_info(fmcw_handle* h, int key, int64_t* value) {
     case FMCW_INFO_WINDOW_SATURATIONS: *value = h->last_status[0]; return FMCW_OK;
     case FMCW_INFO_WORD_SATURATIONS: *value = h->last_status[1]; return FMCW_OK;
     case FMCW_INFO_CFAR2D_STEPS: *value = h->cfar2_steps_last; return FMCW_OK;
-    case FMCW_INFO_GRAPH_REPLAYS: *value = (int64_t)h->graph_replays; return FMCW_OK;
 #if FMCW_LAB
     case 100:  // FMCW_K3_COUNT builds: 2-D CFAR screen survivors / candidates since fmcw_cfar's zeroing
     case 101: {

@@ -29,8 +29,8 @@ COMM_ID_BYTES = 128
 K_RANGE, K_DOPPLER, K_CFAR2D, K_COMPACT, K_COUNT = 0, 1, 2, 3, 4
 KERNEL_NAMES = ("k_range", "k_doppler", "k_cfar", "k_compact")
 INFO_CHUNK, INFO_RANGE_KERNEL, INFO_WINDOW_SATURATIONS, INFO_WORD_SATURATIONS = 4, 6, 7, 8
-INFO_CFAR2D_STEPS, INFO_GRAPH_REPLAYS = 9, 10
-PARAM_CFAR2D_STEPS, PARAM_GRAPHS = 1, 2   # fmcw_set_param keys
+INFO_CFAR2D_STEPS = 9
+PARAM_CFAR2D_STEPS = 1   # fmcw_set_param keys
 # FMCW_INFO_RANGE_KERNEL 0..3 (1 = round 2's k_range2, retired in ABI 6)
 RANGE_KERNELS = ("k_range", "k_range2 (retired)", "k_range_sq", "k_range_px")
 STATUS_WORDS = 4      # FMCW_STATUS_WORDS: n_dets_dev = found, lost, window / word saturations

@@ -267,9 +267,8 @@ class RadarCore:
 
     def set_param(self, key: str, value: int) -> None:
         """fmcw_set_param (tuning; results never depend on it): "cfar2d_steps" = 2-D CFAR steps
-        per strip, 0 = the library's cost model; "graphs" = 1 (default) replays a repeated
-        enqueue argument set as a captured hipGraph, 0 launches every kernel directly."""
-        k = {"cfar2d_steps": L.PARAM_CFAR2D_STEPS, "graphs": L.PARAM_GRAPHS}[key]
+        per strip, 0 = the library's cost model."""
+        k = {"cfar2d_steps": L.PARAM_CFAR2D_STEPS}[key]
         L.check(self._lib.fmcw_set_param(self._h, k, int(value)))
 
     def info(self, key: str) -> int:
@@ -277,11 +276,10 @@ class RadarCore:
         2 k_range_sq, 3 k_range_px; 1 retired), "window_saturations" / "word_saturations" (status
         words 2 / 3 of the last process() call; window_saturations is the sticky status_overflow
         of radar_core.vhd:447-456 as a count), "cfar2d_steps" (strip length of the last 2-D CFAR
-        launch), "graph_replays" (enqueue calls served by a captured graph)."""
+        launch)."""
         k = {"chunk": L.INFO_CHUNK, "range_kernel": L.INFO_RANGE_KERNEL,
              "window_saturations": L.INFO_WINDOW_SATURATIONS,
-             "word_saturations": L.INFO_WORD_SATURATIONS, "cfar2d_steps": L.INFO_CFAR2D_STEPS,
-             "graph_replays": L.INFO_GRAPH_REPLAYS}[key]
+             "word_saturations": L.INFO_WORD_SATURATIONS, "cfar2d_steps": L.INFO_CFAR2D_STEPS}[key]
         v = C.c_int64(0)
         L.check(self._lib.fmcw_get_info(self._h, k, C.byref(v)))
         return int(v.value)

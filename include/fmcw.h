@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define FMCW_ABI_VERSION 7  /* 2: fmcw_config grew compat_rtl, range_shift (27 words, 108 B);
+#define FMCW_ABI_VERSION 6  /* 2: fmcw_config grew compat_rtl, range_shift (27 words, 108 B);
                                3: + spectrum_dtype (28 words, 112 B);
                                4: FMCW_K_COUNT 5 -> 6, FMCW_INFO_PAIR_CHUNK;
                                5: n_dets_dev holds FMCW_STATUS_WORDS (4) words (saturation
@@ -66,9 +66,7 @@ extern "C" {
                                   fmcw_comm_create takes wire_cap, fmcw_gather_dets det_cap;
                                6: fmcw_set_param (FMCW_PARAM_CFAR2D_STEPS), FMCW_INFO_CFAR2D_STEPS;
                                   range-kernel id 1 (k_range2) retired; the library reads no
-                                  environment variable;
-                               7: FMCW_PARAM_GRAPHS (fmcw_enqueue replays a repeated argument set
-                                  as a captured hipGraph, default on), FMCW_INFO_GRAPH_REPLAYS */
+                                  environment variable */
 
 typedef enum {
   FMCW_OK = 0,
@@ -192,20 +190,13 @@ typedef enum {
  * 1 (round 2's k_range2) is retired.  FMCW_INFO_WINDOW_SATURATIONS / FMCW_INFO_WORD_SATURATIONS:
  * status words 2 / 3 of the last fmcw_process call (fmcw_enqueue callers read them from
  * n_dets_dev).  FMCW_INFO_CFAR2D_STEPS: the strip length (workgroup steps) of the handle's last
- * 2-D CFAR launch (0 before the first).  FMCW_INFO_GRAPH_REPLAYS: fmcw_enqueue calls served by
- * a captured graph since fmcw_create. */
+ * 2-D CFAR launch (0 before the first). */
 typedef enum { FMCW_INFO_CHUNK = 4, FMCW_INFO_RANGE_KERNEL = 6, FMCW_INFO_WINDOW_SATURATIONS = 7,
-               FMCW_INFO_WORD_SATURATIONS = 8, FMCW_INFO_CFAR2D_STEPS = 9,
-               FMCW_INFO_GRAPH_REPLAYS = 10 } fmcw_info_key;
+               FMCW_INFO_WORD_SATURATIONS = 8, FMCW_INFO_CFAR2D_STEPS = 9 } fmcw_info_key;
 
 /* fmcw_set_param keys (tuning; results never depend on them).  FMCW_PARAM_CFAR2D_STEPS: steps
- * (4-wave-tile workgroup tiles) per 2-D CFAR strip, 0 = the library's cost model (default).
- * FMCW_PARAM_GRAPHS: 1 (default) = the second and later fmcw_enqueue calls with the same
- * (cube, n_frames, rd_map, dets, det_cap, n_dets_dev) replay one hipGraph captured from the
- * call's launch sequence (up to 8 argument sets per handle, least recently used evicted); 0 =
- * every call launches its kernels one by one.  Either setting clears the handle's graphs.
- * Profiling (fmcw_set_profiling) always launches directly. */
-typedef enum { FMCW_PARAM_CFAR2D_STEPS = 1, FMCW_PARAM_GRAPHS = 2 } fmcw_param_key;
+ * (4-wave-tile workgroup tiles) per 2-D CFAR strip, 0 = the library's cost model (default). */
+typedef enum { FMCW_PARAM_CFAR2D_STEPS = 1 } fmcw_param_key;
 
 /* Status words of fmcw_enqueue / fmcw_cfar (n_dets_dev). */
 #define FMCW_STATUS_WORDS 4

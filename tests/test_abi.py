@@ -38,9 +38,7 @@ def test_header_enums_match_binding():
     assert enum["FMCW_INFO_WORD_SATURATIONS"] == L.INFO_WORD_SATURATIONS
     assert enum["FMCW_INFO_CFAR2D_STEPS"] == L.INFO_CFAR2D_STEPS
     assert enum["FMCW_PARAM_CFAR2D_STEPS"] == L.PARAM_CFAR2D_STEPS
-    assert enum["FMCW_INFO_GRAPH_REPLAYS"] == L.INFO_GRAPH_REPLAYS
-    assert enum["FMCW_PARAM_GRAPHS"] == L.PARAM_GRAPHS
-    assert re.search(r"#define FMCW_ABI_VERSION 7\b", src)
+    assert re.search(r"#define FMCW_ABI_VERSION 6\b", src)
     assert int(re.search(r"#define FMCW_STATUS_WORDS (\d+)", src).group(1)) == L.STATUS_WORDS
 
 
@@ -65,7 +63,7 @@ def test_gfx950_code_object_present(lib_built):
 
 def test_struct_layouts():
     assert C.sizeof(L.FmcwDet) == 16
-    assert C.sizeof(L.FmcwConfig) == 28 * 4          # ABI 3-7 (fmcw.h FMCW_ABI_VERSION)
+    assert C.sizeof(L.FmcwConfig) == 28 * 4          # ABI 3-6 (fmcw.h FMCW_ABI_VERSION)
     assert L.FmcwDet.range.offset == 4 and L.FmcwDet.mag.offset == 8
 
 
@@ -79,7 +77,7 @@ def test_defaults_mirror_radar_core(lib_built):
             cfg.cfar2d_scale_max, cfg.cfar2d_scale_override) == (75, 2, 4, 6, 0)
     assert (cfg.cfar1d_ref, cfg.cfar1d_guard, cfg.cfar1d_rank) == (8, 2, 12)
     assert cfg.cfar1d_alpha == 4.0
-    assert lib_built.fmcw_abi_version() == 7
+    assert lib_built.fmcw_abi_version() == 6
     assert (cfg.compat_rtl, cfg.range_shift, cfg.spectrum_dtype) == (0, 0, L.SPEC_F32)
     assert b"gfx950" in lib_built.fmcw_version()
 
@@ -128,7 +126,6 @@ def test_fp16_spectrum_excludes_q15_window(lib_built):
 
 def test_set_param_rejects_bad_arguments(lib_built):
     assert lib_built.fmcw_set_param(None, L.PARAM_CFAR2D_STEPS, 4) == L.FMCW_EINVAL
-    assert lib_built.fmcw_set_param(None, L.PARAM_GRAPHS, 1) == L.FMCW_EINVAL
 
 
 def test_release_library_reads_no_environment():

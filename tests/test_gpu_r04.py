@@ -95,28 +95,3 @@ def test_cfar2d_dense_candidates_exact_count():
     want = CB.cfar(m, O.Cfar2D(), threads=16)
     assert len(want) > nf * ns * nc // 12
     np.testing.assert_array_equal(got, want)
-
-
-@pytest.mark.parametrize("cfar,nrx", [("os2d", 1), ("os1d", 2)])
-def test_enqueue_graph_replay_matches_direct(cfar, nrx):
-    """FMCW_PARAM_GRAPHS (default on): the second fmcw_enqueue with the same arguments is captured
-    into a hipGraph and later ones replay it.  fmcw_process reuses its staging buffers, so
-    repeated process() calls on one handle take that path; maps and detection lists must equal a
-    handle that launches every kernel directly (graphs 0), call by call, on different data."""
-    ns, nc, nf = 1024, 128, 5
-    cubes = [synth.frames(nf, ns, nc, nrx, "random_target", seed=60 + i) for i in range(4)]
-    kw = dict(N_RANGE=ns, N_DOPPLER=nc, N_RX=nrx, cfar=cfar, max_frames=nf, chunk_frames=2)
-    with RadarCore(**kw) as g, RadarCore(**kw) as d:
-        d.set_param("graphs", 0)
-        for cube in cubes:
-            og, od = g.process(cube), d.process(cube)
-            np.testing.assert_array_equal(og.rd_map, od.rd_map)
-            np.testing.assert_array_equal(og.dets, od.dets)
-            assert og.n_dets == od.n_dets >= nf
-        assert g.info("graph_replays") == len(cubes) - 1 and d.info("graph_replays") == 0
-        if cfar == "os2d":
-            assert g.info("cfar2d_steps") == d.info("cfar2d_steps") > 0
-        g.set_param("cfar2d_steps", 1)  # clears the captured graphs: the next call runs directly
-        og = g.process(cubes[0])
-        np.testing.assert_array_equal(og.dets, d.process(cubes[0]).dets)
-        assert g.info("graph_replays") == len(cubes) - 1
