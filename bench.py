@@ -18,8 +18,8 @@ Launch: `python bench.py [--gpus N --steps K --warmup W]`, or for N > 1
  --master-port P bench.py --gpus N ...`.  Rank 0 prints ONE JSON line.
 
 roofline: the dominant kernel's algorithmic bytes per launch / its average launch duration,
-from HIP events the library records on the launch stream (fmcw_set_profiling) over a
-profiled repeat of the timed steps.  traffic: HBM bytes per launch from rocprofv3 PMC passes
+from HIP events the library records on the launch stream (fmcw_set_profiling: the dispatches'
+own begin / end timestamps, hipExtLaunchKernelGGL) over a profiled repeat of the timed steps.  traffic: HBM bytes per launch from rocprofv3 PMC passes
 (profiles/pmc_r04.json, per frame x the launch's mean frames; tools/pmc_summary.py), or null.
 The 2-D CFAR (k_cfar2d) is bound by VALU work, not bytes: its roofline is SQ_INSTS_VALU per
 launch (same profile file) / launch time against the chip's VALU issue rate (2 wave-instructions

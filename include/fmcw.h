@@ -277,9 +277,10 @@ int fmcw_gather_pack_for_test(const fmcw_det* dets_dev, size_t det_cap, const ui
 int fmcw_gather_compact_for_test(const fmcw_det* msgs_dev, int n_ranks, size_t wire_cap,
                                  fmcw_det* out_dev, uint32_t* out_n_dev, void* stream);
 
-/* Profiling: when enabled, fmcw_enqueue brackets each kernel launch with hipEvents on
- * its stream; fmcw_kernel_times synchronises and returns, per fmcw_kernel_id, the summed
- * milliseconds and the number of launches since the last reset. */
+/* Profiling: when enabled, every stage launch carries hipEvents on its stream that take the
+ * dispatches' own begin / end timestamps (hipExtLaunchKernelGGL: the first launch of a stage
+ * starts the event pair, its last one stops it); fmcw_kernel_times synchronises and returns, per
+ * fmcw_kernel_id, the summed milliseconds and the number of stage launches since the last reset. */
 int fmcw_set_profiling(fmcw_handle* h, int enable);
 int fmcw_set_param(fmcw_handle* h, int key, int64_t value);
 int fmcw_get_info(fmcw_handle* h, int key, int64_t* value);
