@@ -5,7 +5,8 @@ Builds each workload's linear map once through the whole path (bench.py's synthe
 then runs fmcw_cfar on it repeatedly with the library's per-kernel HIP-event timing and prints
 one JSON line per (workload, scale override): mean k_cfar2d time per launch, launches, the
 detection count and a hash of the ordered detection list (A/B variants must agree bit for bit).
-usage: python tools/cfar2d_bench.py [--workloads c3,c5] [--iters 20] [--ovr 0,7]
+usage: python tools/cfar2d_bench.py [--workloads c3,c5] [--iters 20] [--ovr 0,7] [--steps 0,16,32]
+(--steps: strip lengths through fmcw_set_param, 0 = the library's cost model)
 (FMCW_LIB=lib/var_<name>.so selects a variant library built by tools/build_variants.sh)"""
 import argparse
 import hashlib
@@ -26,6 +27,7 @@ def main():
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--ovr", default="0,7")
+    ap.add_argument("--steps", default="0")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -51,10 +53,11 @@ def main():
             core.enqueue(cube, F, rd_map, dets, cap, nd, stream=stream)
             torch.cuda.synchronize()
         del cube
-        for ovr in [int(x) for x in a.ovr.split(",")]:
+        for ovr, st in [(int(o), int(x)) for o in a.ovr.split(",") for x in a.steps.split(",")]:
             with RadarCore(N_RANGE=ns, N_DOPPLER=nc, N_RX=nrx, in_dtype=g["dtype"], cfar="os2d",
                            max_frames=F, cfar_scale_ovr=ovr) as core:
                 cnt = {}
+                core.set_param("cfar2d_steps", st)
                 if os.environ.get("FMCW_K3_COUNTS"):  # a FMCW_LAB + FMCW_K3_COUNT variant library
                     import ctypes as C
                     def rd(k):
@@ -76,7 +79,8 @@ def main():
                 n = int(nd[0].item())
                 h = hashlib.sha1(dets[:n].cpu().numpy().tobytes()).hexdigest()[:16]
                 ms, calls = kt["k_cfar"]
-                print(json.dumps({"workload": w, "ovr": ovr, "frames": F, "k_cfar2d_us_per_launch":
+                print(json.dumps({"workload": w, "ovr": ovr, "steps": core.info("cfar2d_steps"), "frames": F,
+                                  "k_cfar2d_us_per_launch":
                                   round(1e3 * ms / max(1, calls), 2), "launches": calls,
                                   "frames_per_launch": F * a.iters / max(1, calls),
                                   "us_per_frame": round(1e3 * ms / (F * a.iters), 2),

@@ -2,7 +2,7 @@
 // BASELINE config 5's map geometry (8192 range x 1024 Doppler, 2-D CFAR with the reference
 // window of rtl/src/os_cfar_2d.vhd as instantiated at radar_core.vhd:376-382).
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -o tools/k3_lab tools/k3_lab.hip
-// Run:   tools/k3_lab [frames=16] [reps=5] [ns=8192] [nc=1024] [nrx=1]   (nc 1024 / 512 / 256; nrx > 1:
+// Run:   tools/k3_lab [frames=16] [reps=5] [ns=8192] [nc=1024] [nrx=1] [steps=0 (cost model)]   (nc 1024 / 512 / 256; nrx > 1:
 //        the cells are the non-coherent sum over nrx complex-Gaussian channels, as config 3's NCI map)
 // Synthetic map: Rayleigh noise (|complex Gaussian|) plus point targets with Hamming-like
 // sidelobes; every variant's detection list (per tile: count + records) must equal the
@@ -92,6 +92,8 @@ int steps_model(int nf, int tpf, int grid, int tr, int hr) {  // = fmcw_api.hip 
   return best;
 }
 
+static int g_steps = 0;  // strip length (argv[6]; 0 = the library's cost model)
+
 template <int NC>
 int run(int nf, int reps, int ns, int nrx) {
   const float* map = nullptr;
@@ -113,7 +115,7 @@ int run(int nf, int reps, int ns, int nrx) {
   vars.push_back({"k_cfar2d + decide + emit (production)", reinterpret_cast<const void*>(k_cfar2d<NC, 6, 2, 5, 1>),
                   cfar2d_smem_bytes<NC>(a.hr), [&](int grid, size_t smem, int n_strips, int steps, DetSink sink,
                                                    Cfar2Cands cands) {
-                    hipMemsetAsync(cands.ctr, 0, 8, 0);
+                    hipMemsetAsync(cands.ctr, 0, 16, 0);
                     hipLaunchKernelGGL((k_cfar2d<NC, 6, 2, 5, 1>), dim3(grid), dim3(256), smem, 0, map, ns, n_strips,
                                        steps, 0, 0, a, sink, cands);
                     hipLaunchKernelGGL(k_cfar2d_decide<NC>, dim3(1024), dim3(256), 0, 0, map, ns, a, cands);
@@ -178,7 +180,7 @@ int run(int nf, int reps, int ns, int nrx) {
     CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, v.fn, 256, smem));
     const int grid_max = std::max(1, per_cu) * n_cu;
     const int tpf = (ns / WR + 3) / 4;
-    const int steps = steps_model(nf, tpf, grid_max, WR * 4, a.hr);
+    const int steps = g_steps > 0 ? std::min(g_steps, tpf) : steps_model(nf, tpf, grid_max, WR * 4, a.hr);
     const int n_strips = nf * ((tpf + steps - 1) / steps);
     const int grid = std::min(n_strips, grid_max);
     CK(hipMemset(sink.counter, 0, 16));
@@ -239,6 +241,7 @@ int main(int argc, char** argv) {
   const int ns = argc > 3 ? std::atoi(argv[3]) : 8192;
   const int nc = argc > 4 ? std::atoi(argv[4]) : 1024;
   const int nrx = argc > 5 ? std::atoi(argv[5]) : 1;
+  g_steps = argc > 6 ? std::atoi(argv[6]) : 0;
   switch (nc) {
     case 1024: return run<1024>(nf, reps, ns, nrx);
     case 512: return run<512>(nf, reps, ns, nrx);
