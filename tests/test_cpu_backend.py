@@ -47,3 +47,16 @@ def _oracle(m, cf, f):
 def test_host_info_fields():
     info = CB.host_info()
     assert info["nproc"] >= 1 and info["affinity"] >= 1 and "cpu_model" in info
+
+
+def test_c_backend_under_host_sanitizers():
+    """oracle/fmcw_cpu.c under AddressSanitizer + UBSan (tools/oracle_asan.sh): whole path and
+    CFAR alone at five geometries, 1-D and 2-D, detection capacities shorter than the list."""
+    import shutil
+    import subprocess
+    from conftest import REPO
+    if not shutil.which("gcc"):
+        pytest.skip("no gcc")
+    r = subprocess.run(["bash", str(REPO / "tools" / "oracle_asan.sh")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    assert "ok (" in r.stdout
