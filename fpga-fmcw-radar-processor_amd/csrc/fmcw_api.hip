@@ -40,32 +40,9 @@ k_det_scan_blocks(const uint32_t* __restrict__ wg_count, uint32_t* __restrict__ 
   if (threadIdx.x == 0) block_sum[blockIdx.x] = (uint32_t)total;
 }
 
-// level 2: one workgroup scans the block sums in place (-> block offsets) and the total
-__global__ void __launch_bounds__(1024)
-k_det_scan_top(uint32_t* __restrict__ block_sum, int nb, uint32_t* __restrict__ n_dets,
-               const uint32_t* __restrict__ dropped) {
-  __shared__ int s_wave[1024 / 64 + 2];
-  const int per = (nb + 1023) / 1024;
-  const int b = threadIdx.x * per;
-  const int e = min(b + per, nb);
-  uint32_t s = 0;
-  for (int i = b; i < e; ++i) s += block_sum[i];
-  int total;
-  uint32_t run = (uint32_t)block_excl_scan<1024>((int)s, s_wave, total);
-  for (int i = b; i < e; ++i) {
-    const uint32_t c = block_sum[i];
-    block_sum[i] = run;
-    run += c;
-  }
-  if (threadIdx.x == 0) {
-    n_dets[0] = (uint32_t)total;  // every detection found
-    n_dets[1] = *dropped;         // of which not stored (handle scratch exhausted)
-  }
-}
-
-// Start of a call: the handle's detection counters, the caller's status words and the 2-D CFAR
-// launches' candidate counters, zeroed by one launch (two hipMemsetAsync fills cost ~12 us per
-// call, 1 % of a config-2 step).
+// Zeroing of up to three word arrays in one launch (two hipMemsetAsync fills cost ~12 us): the
+// caller's status words of a call without a CFAR, and the handle's per-call counters when the
+// previous call did not re-arm them (k_det_finish).
 __global__ void k_zero_words(uint32_t* __restrict__ a, int na, uint32_t* __restrict__ b, int nb,
                              uint32_t* __restrict__ c, int nc) {
   for (int i = threadIdx.x; i < max(na, max(nb, nc)); i += blockDim.x) {
@@ -75,20 +52,60 @@ __global__ void k_zero_words(uint32_t* __restrict__ a, int na, uint32_t* __restr
   }
 }
 
-// One lane per tile; a tile with more than 8 detections (a target's row) is copied by the
-// whole wave, 64 records per step, so one hot tile does not serialise the kernel.
-__global__ void k_det_copy(const fmcw_det* __restrict__ scratch, uint32_t scratch_cap,
-                           const uint32_t* __restrict__ wg_base, const uint32_t* __restrict__ wg_count,
-                           const uint32_t* __restrict__ wg_off, const uint32_t* __restrict__ block_off,
-                           int n, fmcw_det* __restrict__ out, uint32_t cap) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int lane = threadIdx.x & 63;
+// Level 2 and the copy in one launch (round 4; before: a one-workgroup scan of the block sums,
+// then the copy).  Workgroup w covers tiles 256 w .. 256 w + 255, all inside level-1 block
+// (256 w) >> 10, and sums the level-1 block totals before that block itself (<= n / 1024 of them,
+// L2-resident) for its offset.  One lane per tile; a tile with more than 8 detections (a target's
+// row) is copied by the whole wave, 64 records per step, so one hot tile does not serialise the
+// kernel.  Workgroup 0 also writes the status words -- [0] every detection found, [1] of which
+// not stored, [2] / [3] the saturation counts the call's K1 / K2 accumulated in the handle's `sat`
+// -- and re-arms the handle's per-call counters (overflow use, drops, saturations, the 2-D CFAR
+// launches' candidate counters) for the next call: every kernel that uses them ran before this one.
+__global__ void __launch_bounds__(256)
+k_det_finish(const fmcw_det* __restrict__ scratch, uint32_t scratch_cap, const uint32_t* __restrict__ wg_base,
+             const uint32_t* __restrict__ wg_count, const uint32_t* __restrict__ wg_off,
+             const uint32_t* __restrict__ block_sum, int nb, int n, fmcw_det* __restrict__ out, uint32_t cap,
+             uint32_t* __restrict__ n_dets, uint32_t* __restrict__ counter, uint32_t* __restrict__ sat,
+             uint32_t* __restrict__ k3_ctr, int n_k3) {
+  __shared__ uint32_t s_red[2][4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int jb = (int)((blockIdx.x * 256u) >> 10);  // this workgroup's level-1 block
+  uint32_t pre = 0, all = 0;
+  for (int j = threadIdx.x; j < nb; j += 256) {
+    const uint32_t v = block_sum[j];
+    pre += j < jb ? v : 0u;
+    all += v;
+  }
+#pragma unroll
+  for (int x = 32; x >= 1; x >>= 1) {
+    pre += (uint32_t)__shfl_xor((int)pre, x, 64);
+    all += (uint32_t)__shfl_xor((int)all, x, 64);
+  }
+  if (lane == 0) {
+    s_red[0][wv] = pre;
+    s_red[1][wv] = all;
+  }
+  __syncthreads();
+  const uint32_t P = s_red[0][0] + s_red[0][1] + s_red[0][2] + s_red[0][3];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    n_dets[0] = s_red[1][0] + s_red[1][1] + s_red[1][2] + s_red[1][3];
+    n_dets[1] = counter[1];
+    n_dets[2] = sat ? sat[0] : 0u;
+    n_dets[3] = sat ? sat[1] : 0u;
+    counter[0] = 0u;
+    counter[1] = 0u;
+    if (sat) sat[0] = sat[1] = 0u;
+  }
+  if (blockIdx.x == 0)
+    for (int k = threadIdx.x; k < n_k3; k += 256) k3_ctr[k] = 0u;
+  if (!out) return;
+  const int i = blockIdx.x * 256 + threadIdx.x;
   uint32_t c = 0, b = 0, o = 0;
   if (i < n) {
     c = wg_count[i];
     if (c) {
       b = wg_base[i];
-      o = block_off[i >> 10] + wg_off[i];
+      o = P + wg_off[i];
     }
   }
   if (c <= 8)
@@ -187,6 +204,11 @@ struct fmcw_handle {
   uint32_t slot_cap = 32;  // detections per tile slot (sized in fmcw_create; more -> overflow)
   uint32_t ovf_base = 0;   // first overflow entry
   uint32_t* counter = nullptr;  // [0] overflow entries used, [1] dropped
+  uint32_t* sat = nullptr;      // [0] window, [1] word saturations of the current call (status words 2, 3)
+  // the per-call device counters (counter[0..1], sat, k3_ctr) are zero: re-armed by the previous
+  // call's k_det_finish (or at fmcw_create); a call that stopped early leaves this false and the
+  // next one zeroes them first
+  bool counters_armed = false;
   uint32_t* wg_base = nullptr;
   uint32_t* wg_count = nullptr;
   uint32_t* wg_off = nullptr;
@@ -458,6 +480,18 @@ int cfar2_steps_model(int nf, int tpf, int grid, int tr, int hr) {
   return best;
 }
 
+// Zero the per-call counters unless the previous call's k_det_finish left them armed; the flag
+// drops until this call's k_det_finish is enqueued.
+int arm_counters(fmcw_handle* h, hipStream_t s) {
+  if (!h->counters_armed) {
+    hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(256), 0, s, h->counter, 2, h->sat, 2, h->k3_ctr,
+                       2 * h->k3_launches);
+    if (int rc = check_launch("k_zero_words")) return rc;
+  }
+  h->counters_armed = false;
+  return FMCW_OK;
+}
+
 constexpr size_t kCfar2Batch = 16;  // frames per 2-D CFAR launch on the caller's map (at least)
 constexpr int kCfar2DecideGrid = 1024;  // K3b workgroups (4 waves each, one candidate per wave at a time)
 constexpr int kCfar2EmitGrid = 256;     // K3c workgroups (one wave tile per wave at a time)
@@ -508,26 +542,20 @@ int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipS
 }
 
 int launch_det_finish(fmcw_handle* h, size_t n_frames, fmcw_det* dets, size_t det_cap,
-                      uint32_t* n_dets_dev, hipStream_t s) {
+                      uint32_t* n_dets_dev, uint32_t* sat, hipStream_t s) {
   const int n = (int)(n_frames * tiles_per_frame(h));
   const int nb = (n + 1023) / 1024;
   ProfScope ps(h, FMCW_K_COMPACT);
-  const bool copy = dets && det_cap;
   launch_k(ps, false, k_det_scan_blocks, dim3(nb), dim3(1024), 0u, s, (const uint32_t*)h->wg_count, h->wg_off, n,
            h->block_sum);
-  launch_k(ps, !copy, k_det_scan_top, dim3(1), dim3(1024), 0u, s, h->block_sum, nb, n_dets_dev,
-           (const uint32_t*)(h->counter + 1));
-  int rc = check_launch("k_det_scan");
-  if (rc) return rc;
-  if (copy) {
-    // entries past the handle's scratch capacity are never stored: clip to it as well
-    const uint32_t cap = (uint32_t)std::min<size_t>(det_cap, h->det_scratch_cap);
-    launch_k(ps, true, k_det_copy, dim3((n + 255) / 256), dim3(256), 0u, s, (const fmcw_det*)h->det_scratch,
-             h->det_scratch_cap, (const uint32_t*)h->wg_base, (const uint32_t*)h->wg_count,
-             (const uint32_t*)h->wg_off, (const uint32_t*)h->block_sum, n, dets, cap);
-    rc = check_launch("k_det_copy");
-  }
-  return rc;
+  // entries past the handle's scratch capacity are never stored: clip to it as well
+  const bool copy = dets && det_cap;
+  const uint32_t cap = copy ? (uint32_t)std::min<size_t>(det_cap, h->det_scratch_cap) : 0u;
+  launch_k(ps, true, k_det_finish, dim3(copy ? (n + 255) / 256 : 1), dim3(256), 0u, s,
+           (const fmcw_det*)h->det_scratch, h->det_scratch_cap, (const uint32_t*)h->wg_base,
+           (const uint32_t*)h->wg_count, (const uint32_t*)h->wg_off, (const uint32_t*)h->block_sum, nb, n,
+           copy ? dets : (fmcw_det*)nullptr, cap, n_dets_dev, h->counter, sat, h->k3_ctr, 2 * h->k3_launches);
+  return check_launch("k_det_scan_blocks / k_det_finish");
 }
 
 // 2^-range_shift for the Q15 window path (the fp32 window tables carry it otherwise)
@@ -723,6 +751,7 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   }
   ALLOC(h->det_scratch, (size_t)h->det_scratch_cap * sizeof(fmcw_det));
   ALLOC(h->counter, 16);
+  ALLOC(h->sat, 8);
   ALLOC(h->n_dets_tmp, 16);
   ALLOC(h->wg_base, h->n_wg_max * sizeof(uint32_t));
   ALLOC(h->wg_count, h->n_wg_max * sizeof(uint32_t));
@@ -767,7 +796,7 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
 int fmcw_destroy(fmcw_handle* h) {
   if (!h) return FMCW_OK;
   hipSetDevice(h->cfg.device_id);
-  void* ptrs[] = {h->win_r, h->win_d, h->inter, h->lin_scratch, h->det_scratch, h->counter,
+  void* ptrs[] = {h->win_r, h->win_d, h->inter, h->lin_scratch, h->det_scratch, h->counter, h->sat,
                   h->n_dets_tmp, h->wg_base, h->wg_count, h->wg_off, h->block_sum,
                   h->stage_cube, h->stage_map, h->stage_dets, h->cand_cell, h->cand_thr,
                   h->cand_tiles, h->k3_ctr};
@@ -798,15 +827,19 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
   const size_t in_frame_bytes = cube_bytes(c, 1);
   const Cfar1DArgs cf1 = cfar1_args(c);
   const bool q15 = c.window == FMCW_WIN_Q15_RTL;
-  // status words 2 / 3 (saturations) are counted atomically by the kernels that can saturate
-  uint32_t* const status = n_dets_dev ? n_dets_dev + 2 : nullptr;
+  // status words 2 / 3 (saturations) are counted atomically by the kernels that can saturate: into
+  // the handle's `sat` words, which the call's last kernel (k_det_finish) reports and re-arms
+  // with the other per-call counters; without a CFAR there is no such kernel, and the caller's
+  // words are zeroed and counted into directly
+  const bool cfar = c.cfar_kind != FMCW_CFAR_NONE;
+  uint32_t* const status = cfar ? h->sat : n_dets_dev ? n_dets_dev + 2 : nullptr;
   int rc;
-  if (c.cfar_kind != FMCW_CFAR_NONE || n_dets_dev) {
-    hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(256), 0, s, c.cfar_kind != FMCW_CFAR_NONE ? h->counter : nullptr, 2,
-                       n_dets_dev, FMCW_STATUS_WORDS, h->k3_ctr, 2 * h->k3_launches);
-    h->k3_launch_idx = 0;
+  if (!cfar && n_dets_dev) {
+    hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(256), 0, s, nullptr, 0, n_dets_dev, FMCW_STATUS_WORDS, nullptr, 0);
     if ((rc = check_launch("k_zero_words"))) return rc;
   }
+  if (cfar && (rc = arm_counters(h, s))) return rc;
+  h->k3_launch_idx = 0;
 
   // Chunks of h->chunk frames: K1 -> corner-turned spectrum -> K2 (+ K3)
   const size_t n_chunks = (n_frames + h->chunk - 1) / h->chunk;
@@ -855,7 +888,10 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
       }
     }
   }
-  if (c.cfar_kind != FMCW_CFAR_NONE) return launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, s);
+  if (cfar) {
+    if ((rc = launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, h->sat, s))) return rc;
+    h->counters_armed = true;  // k_det_finish re-arms them on the device, in stream order
+  }
   return FMCW_OK;
 }
 
@@ -959,13 +995,13 @@ int fmcw_cfar(fmcw_handle* h, const float* map, size_t n_frames, fmcw_det* dets,
   if (n_frames < 1 || n_frames > c.max_frames) return fail(FMCW_EINVAL, "n_frames out of range");
   HIP_TRY(hipSetDevice(c.device_id));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(256), 0, s, h->counter, 2, n_dets_dev, FMCW_STATUS_WORDS, h->k3_ctr,
-                     2 * h->k3_launches);
-  if (int rc0 = check_launch("k_zero_words")) return rc0;
+  if (int rc0 = arm_counters(h, s)) return rc0;
   h->k3_launch_idx = 0;
   int rc = launch_cfar(h, map, (int)n_frames, 0, s);
   if (rc) return rc;
-  return launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, s);
+  if ((rc = launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, nullptr, s))) return rc;
+  h->counters_armed = true;
+  return FMCW_OK;
 }
 
 int fmcw_set_profiling(fmcw_handle* h, int enable) {
