@@ -95,3 +95,24 @@ def test_cfar2d_dense_candidates_exact_count():
     want = CB.cfar(m, O.Cfar2D(), threads=16)
     assert len(want) > nf * ns * nc // 12
     np.testing.assert_array_equal(got, want)
+
+
+def test_counters_rearmed_across_calls():
+    """The per-call device counters (overflow use, drops, saturations, the 2-D CFAR launches'
+    candidate counters) are re-armed by each call's last kernel (k_det_finish), not zeroed at the
+    next call's start: alternate fmcw_cfar stage calls on a map that fills the overflow region
+    (every third cell detects) with whole-path calls on a cube, on one handle, and check every
+    call against the oracle."""
+    ns, nc, nf = 512, 256, 2
+    rng = np.random.default_rng(53)
+    m = rng.rayleigh(1.0, (nf, ns, nc)).astype(np.float32)
+    m[:, ::3, ::3] = 50.0
+    want_m = CB.cfar(m, O.Cfar2D(), threads=16)
+    cube = synth.frames(nf, ns, nc, 1, "random_target", seed=54)
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os2d", max_frames=nf) as core:
+        for _ in range(3):
+            got = run_cfar_stage(core, m, cap=1 << 20)
+            np.testing.assert_array_equal(got, want_m)
+            out = core.process(cube)
+            np.testing.assert_array_equal(out.dets, CB.cfar(out.rd_map, O.Cfar2D(), threads=16))
+            assert out.n_dets >= nf and out.window_saturations == 0 and out.word_saturations == 0
