@@ -636,22 +636,17 @@ void fmcw_config_default(fmcw_config* c) {
 }
 
 // Frames per K1 -> K2 chunk when the caller leaves chunk_frames at 0.  The corner-turned
-// spectrum of a chunk is written by K1 and read back by K2 right after; kept to ~3/4 of the
+// spectrum of a chunk is written by K1 and read back by K2 right after; kept to ~13/16 of the
 // 256 MiB Infinity Cache (MALL), K2's reads hit there.  Measured on config 2 (round 2, 1024
-// frames per step, gpurun_out chunk sweep): K2 0.63 us/frame at 128 frames (256 MiB), 0.57 at
-// 96, 0.55 at 108-120, 0.81 from 256 frames up (reads from HBM); K1 unchanged.  Within that,
-// a multiple of the frames one full round of K2's persistent grid covers (config 2: 3072
-// waves / 256 wave tiles = 12 frames, K1 the same), so neither kernel ends on a partial round.
+// frames per step): K2 0.63 us/frame at 128 frames (256 MiB), 0.57 at 96, 0.55 at 108-120, 0.81
+// from 256 frames up (reads from HBM).  Round 4, same box, 3 runs each
+// (profiles/r04/chunk/): 96 frames 807.7-809.6 k frames/s, 104 frames 814.8-820.0 k, 112 frames
+// 810.3-819.5 k -- so 208 MiB, without round 2's rounding down to whole rounds of K2's grid
+// (96 frames), which no longer paid.  Configs 3 / 5 (64 MiB per frame) keep 3 frames.
 uint32_t auto_chunk(const fmcw_handle* h, size_t frame_inter) {
   const fmcw_config& c = h->cfg;
-  constexpr size_t kMallBudget = 192u << 20;
-  size_t ch = std::max<size_t>(1, kMallBudget / frame_inter);
-  const size_t waves = (size_t)h->grid_doppler * (doppler_info(c.n_doppler).NT / 64);
-  const size_t tpf = (size_t)c.n_range / doppler_info(c.n_doppler).WR;
-  if (waves % tpf == 0) {
-    const size_t unit = waves / tpf;  // frames per full K2 round
-    if (ch >= 2 * unit) ch -= ch % unit;
-  }
+  constexpr size_t kMallBudget = 208u << 20;
+  const size_t ch = std::max<size_t>(1, kMallBudget / frame_inter);
   return (uint32_t)std::min<size_t>(c.max_frames, ch);
 }
 
