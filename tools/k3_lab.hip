@@ -2,7 +2,7 @@
 // BASELINE config 5's map geometry (8192 range x 1024 Doppler, 2-D CFAR with the reference
 // window of rtl/src/os_cfar_2d.vhd as instantiated at radar_core.vhd:376-382).
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -o tools/k3_lab tools/k3_lab.hip
-// Run:   tools/k3_lab [frames=16] [reps=5] [ns=8192] [nc=1024] [nrx=1] [steps=0 (cost model)]   (nc 1024 / 512 / 256; nrx > 1:
+// Run:   tools/k3_lab [frames=16] [reps=5] [ns=8192] [nc=1024] [nrx=1] [steps=0 (cost model)] [wg_per_cu=0 (occupancy)]   (nc 1024 / 512 / 256; nrx > 1:
 //        the cells are the non-coherent sum over nrx complex-Gaussian channels, as config 3's NCI map)
 // Synthetic map: Rayleigh noise (|complex Gaussian|) plus point targets with Hamming-like
 // sidelobes; every variant's detection list (per tile: count + records) must equal the
@@ -92,7 +92,8 @@ int steps_model(int nf, int tpf, int grid, int tr, int hr) {  // = fmcw_api.hip 
   return best;
 }
 
-static int g_steps = 0;  // strip length (argv[6]; 0 = the library's cost model)
+static int g_steps = 0;   // strip length (argv[6]; 0 = the library's cost model)
+static int g_per_cu = 0;  // workgroups per CU at most (argv[7]; 0 = occupancy)
 
 template <int NC>
 int run(int nf, int reps, int ns, int nrx) {
@@ -178,6 +179,7 @@ int run(int nf, int reps, int ns, int nrx) {
     CK(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
     int per_cu = 0;
     CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, v.fn, 256, smem));
+    if (g_per_cu > 0) per_cu = std::min(per_cu, g_per_cu);
     const int grid_max = std::max(1, per_cu) * n_cu;
     const int tpf = (ns / WR + 3) / 4;
     const int steps = g_steps > 0 ? std::min(g_steps, tpf) : steps_model(nf, tpf, grid_max, WR * 4, a.hr);
@@ -242,6 +244,7 @@ int main(int argc, char** argv) {
   const int nc = argc > 4 ? std::atoi(argv[4]) : 1024;
   const int nrx = argc > 5 ? std::atoi(argv[5]) : 1;
   g_steps = argc > 6 ? std::atoi(argv[6]) : 0;
+  g_per_cu = argc > 7 ? std::atoi(argv[7]) : 0;
   switch (nc) {
     case 1024: return run<1024>(nf, reps, ns, nrx);
     case 512: return run<512>(nf, reps, ns, nrx);
