@@ -442,16 +442,23 @@ k_range_sq(const void* __restrict__ cube, float2* __restrict__ inter, const floa
       vpasses_mid<N, M, P, V>(lds, t);
       vpass_last<N, LL, P, V>(lds, t, X[q]);
     }
-    // tile stores: lane t holds range bins d = t + P gg + LL m of both chirps
+    // tile stores: lane t holds range bins d = t + P gg + LL m of both chirps; write-through (sc1)
+    // at N <= 4096 as k_range: no dirty spectrum lines left in L2 for the end-of-kernel release
+    // (config 3: K1 58.3-58.7 -> 57.2-57.6 us per launch, 21.7-21.8 k -> 22.0-22.1 k frames/s,
+    // profiles/r04/k1/policy/; nt + sc1 7 % slower)
     const int t = opaque(t0);
     const size_t fbase = (size_t)fr * N * nc;
+    constexpr bool WT = FMCW_K1_WT && N <= 4096;
+    const __amdgpu_buffer_rsrc_t srs = wt_rsrc(inter + fbase, 0xffffffffu);  // one frame's tiles < 4 GiB
 #pragma unroll
     for (int gg = 0; gg < GF; ++gg)
 #pragma unroll
       for (int m = 0; m < RF; ++m) {
         const int d = t + P * gg + LL * m;
-        const size_t off = fbase + ((size_t)(d / RB) * ncb + cb) * (RB * T) + (size_t)(d % RB) * T;
-        st_f4<FMCW_NT_SPEC_ST>(inter + off, make_float4(X[0][gg][m].x, X[0][gg][m].y, X[1][gg][m].x, X[1][gg][m].y));
+        const size_t off = ((size_t)(d / RB) * ncb + cb) * (RB * T) + (size_t)(d % RB) * T;
+        const float4 x = make_float4(X[0][gg][m].x, X[0][gg][m].y, X[1][gg][m].x, X[1][gg][m].y);
+        if constexpr (WT) st_f4_wt(srs, (uint32_t)(off * sizeof(float2)), x);
+        else st_f4<FMCW_NT_SPEC_ST>(inter + fbase + off, x);
       }
   }
 }
