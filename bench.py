@@ -17,6 +17,11 @@ Launch: `python bench.py [--gpus N --steps K --warmup W]`, or for N > 1
 `python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
  --master-port P bench.py --gpus N ...`.  Rank 0 prints ONE JSON line.
 
+Warm-up: the W untimed steps, then more untimed steps until --prewarm-s (0.3 s) of sustained work
+has run, the same count on every rank; "warmup_steps_run" reports the total.  The MI355X reaches
+its steady clocks only after ~0.1 s of load, so timing K=10 steps after 3 warm-up steps (4 ms)
+read 7-10 % low (profiles/r04/warmup/).  --prewarm-s 0 restores the W-only warm-up.
+
 roofline: the dominant kernel's algorithmic bytes per launch / its average launch duration,
 from HIP events the library records on the launch stream (fmcw_set_profiling: the dispatches'
 own begin / end timestamps, hipExtLaunchKernelGGL) over a profiled repeat of the timed steps.  traffic: HBM bytes per launch from rocprofv3 PMC passes
@@ -57,6 +62,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--prewarm-s", type=float, default=0.3,
+                    help="untimed warm-up continues past --warmup steps until this much sustained work has run")
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--frames", type=int, default=0, help="frames per GPU per step (0 = workload default)")
     ap.add_argument("--chunk", type=int, default=0, help="frames per kernel chunk (0 = library auto)")
@@ -244,9 +251,31 @@ def run_workload(name, args, world, rank, dev, primary, pmc, n_cu):
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
         return float(el.item())
 
+    # untimed warm-up: the W steps asked for, then more steps until args.prewarm_s of sustained
+    # work has run (the same number on every rank: the gather is collective).  The MI355X reaches
+    # its steady clocks only after ~0.1 s of load: with 3 warm-up steps (4 ms) the timed steps ran
+    # 7-10 % slower than with 100 (profiles/r04/warmup/).
+    t_w = time.perf_counter()
     for _ in range(warmup):
         step()
     flush()
+    torch.cuda.synchronize(dev)
+    n_warm = warmup
+    if args.prewarm_s > 0:  # same branch on every rank (args are shared)
+        t1 = time.perf_counter()  # one more step, timed on its own: the first ones carry one-time costs
+        step()
+        flush()
+        torch.cuda.synchronize(dev)
+        per = max(time.perf_counter() - t1, 1e-6)
+        n_warm += 1
+        spent = time.perf_counter() - t_w
+        extra = torch.tensor([max(0, int((args.prewarm_s - spent) / per) + 1)], dtype=torch.int64, device=dev)
+        if world > 1:
+            dist.all_reduce(extra, op=dist.ReduceOp.MAX)
+        for _ in range(int(extra.item())):
+            step()
+        flush()
+        n_warm += int(extra.item())
     elapsed = timed(steps)
     st = n_dets.tolist()
     n_det_step = int(st[0])
@@ -266,6 +295,7 @@ def run_workload(name, args, world, rank, dev, primary, pmc, n_cu):
     rec = {
         "metric": "radar frames/sec (range-Doppler+CFAR)",
         "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": steps, "warmup": warmup,
+        "warmup_steps_run": n_warm, "prewarm_s": args.prewarm_s,
         "ms_per_step": round(elapsed / steps * 1e3, 4),
         "dtype": wl["dtype"],
         "config": {"workload": wl["desc"], "frames_per_gpu_step": F, "n_chirps": nc,
@@ -413,7 +443,8 @@ def main():
 
     out = {
         "metric": rec["metric"], "value": rec["value"], "unit": "frames/s", "n_gpus": world,
-        "steps": rec["steps"], "warmup": rec["warmup"], "ms_per_step": rec["ms_per_step"],
+        "steps": rec["steps"], "warmup": rec["warmup"], "warmup_steps_run": rec["warmup_steps_run"],
+        "prewarm_s": rec["prewarm_s"], "ms_per_step": rec["ms_per_step"],
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": rec["dtype"],
         "data": "synthetic (tb_radar_core-style point targets + uniform noise, int16-quantised)",
         "config": rec["config"],
