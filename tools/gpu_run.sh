@@ -26,8 +26,8 @@ for s in "$@"; do
     bench) run bench 600 python bench.py --steps 10 --warmup 3 ;;
     bench_c*) run "$s" 600 python bench.py --workload "${s#bench_}" --steps 10 --warmup 3 --no-cpu-baseline ;;
     prof) run rocprof_stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
-    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
-    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --prewarm-s 0 --no-cpu-baseline ;;
+    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --prewarm-s 0 --no-cpu-baseline ;;
     ablate) run ablate 600 python tools/ablate.py ${ABLATE_ARGS:-} ;;
     ablate_libs)  # every variant build (tools/build_variants.sh), same ablation variants
       for lib in fpga-fmcw-radar-processor_amd/lib/var_*.so; do
@@ -64,10 +64,10 @@ for s in "$@"; do
     # round 3: one default bench command (config 2 + the config-3 / config-5 sub-records), its
     # kernel-trace stats and its three PMC passes (tools/pmc_summary.py normalises per frame)
     prof3) run rocprof3_stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof3" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-h2d ;;
-    pmc3_fetch) run pmc3_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc3_fetch" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
-    pmc3_write) run pmc3_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc3_write" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
-    pmc3_sq) run pmc3_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_ACTIVE_INST_ANY -d "$OUT/pmc3_sq" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
-    pmc3_sq2) run pmc3_sq2 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_SALU -d "$OUT/pmc3_sq2" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-h2d ;;
+    pmc3_fetch) run pmc3_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc3_fetch" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-h2d ;;
+    pmc3_write) run pmc3_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc3_write" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-h2d ;;
+    pmc3_sq) run pmc3_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_ACTIVE_INST_ANY -d "$OUT/pmc3_sq" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-h2d ;;
+    pmc3_sq2) run pmc3_sq2 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_SALU -d "$OUT/pmc3_sq2" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-h2d ;;
     gloo2)  # N = 2 ranks on this one GPU over gloo: a rehearsal of bench.py's launch, barrier and max-over-ranks timing
       run bench_2rank_gloo 600 env FMCW_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline --no-h2d --no-sub --frames 256 ;;
     k3lab) run k3lab_c5 300 tools/k3_lab 16 5 ;;

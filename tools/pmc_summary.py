@@ -61,7 +61,7 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--sq", default=None)
     ap.add_argument("--frames", action="append", default=[], help="workload=frames processed in the run")
-    ap.add_argument("--command", default="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-h2d")
+    ap.add_argument("--command", default="python3 bench.py --steps 2 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-h2d")
     ap.add_argument("--out", default="profiles/pmc_r04.json")
     a = ap.parse_args()
     frames = {k: int(v) for k, v in (x.split("=") for x in a.frames)}
