@@ -103,7 +103,7 @@ def kernel_rooflines(wl, name, F, steps, kt, spectrum, n_cu, pmc):
             "k_doppler": "k_doppler (Doppler FFT + |X|" + (" NCI" if nrx > 1 else "") + " + map"
                          + (" + 1-D CFAR)" if wl["cfar"] == "os1d" else ")"),
             "k_cfar": "k_cfar2d (2-D OS-CFAR, 128 refs, adaptive scale)",
-            "k_compact": "k_det_scan_blocks / k_det_finish (ordered detection list)"}
+            "k_compact": "k_det_list (ordered detection list, one-pass look-back scan)"}
     pw = (pmc.get("workloads") or {}).get(name, {})
     pk = pw.get("kernels", {})
     out = {}

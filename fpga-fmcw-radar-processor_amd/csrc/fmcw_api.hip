@@ -24,25 +24,12 @@ using namespace fmcw;
 // The host side's own small kernels (one translation unit: no instantiation tables).
 namespace fmcw {
 // --------------------------------------------------------------------------------------
-// Detection ordering: exclusive scan over per-workgroup counts (in workgroup = (frame,
-// range) order), then copy each workgroup's run to its final place.
+// Detection ordering: one pass over the per-tile counts (in tile = (frame, range) order) that
+// scans them and copies each tile's run to its final place.
 // --------------------------------------------------------------------------------------
-// level 1: per 1024-entry block, exclusive scan -> wg_off (block-local) + block sums
-__global__ void __launch_bounds__(1024)
-k_det_scan_blocks(const uint32_t* __restrict__ wg_count, uint32_t* __restrict__ wg_off, int n,
-                  uint32_t* __restrict__ block_sum) {
-  __shared__ int s_wave[1024 / 64 + 2];
-  const int i = blockIdx.x * 1024 + threadIdx.x;
-  const int v = i < n ? (int)wg_count[i] : 0;
-  int total;
-  const int e = block_excl_scan<1024>(v, s_wave, total);
-  if (i < n) wg_off[i] = (uint32_t)e;
-  if (threadIdx.x == 0) block_sum[blockIdx.x] = (uint32_t)total;
-}
-
 // Zeroing of up to three word arrays in one launch (two hipMemsetAsync fills cost ~12 us): the
 // caller's status words of a call without a CFAR, and the handle's per-call counters when the
-// previous call did not re-arm them (k_det_finish).
+// previous call did not re-arm them (k_det_list).
 __global__ void k_zero_words(uint32_t* __restrict__ a, int na, uint32_t* __restrict__ b, int nb,
                              uint32_t* __restrict__ c, int nc) {
   for (int i = threadIdx.x; i < max(na, max(nb, nc)); i += blockDim.x) {
@@ -52,62 +39,105 @@ __global__ void k_zero_words(uint32_t* __restrict__ a, int na, uint32_t* __restr
   }
 }
 
-// Level 2 and the copy in one launch (round 4; before: a one-workgroup scan of the block sums,
-// then the copy).  Workgroup w covers tiles 256 w .. 256 w + 255, all inside level-1 block
-// (256 w) >> 10, and sums the level-1 block totals before that block itself (<= n / 1024 of them,
-// L2-resident) for its offset.  One lane per tile; a tile with more than 8 detections (a target's
-// row) is copied by the whole wave, 64 records per step, so one hot tile does not serialise the
-// kernel.  Workgroup 0 also writes the status words -- [0] every detection found, [1] of which
-// not stored, [2] / [3] the saturation counts the call's K1 / K2 accumulated in the handle's `sat`
-// -- and re-arms the handle's per-call counters (overflow use, drops, saturations, the 2-D CFAR
-// launches' candidate counters) for the next call: every kernel that uses them ran before this one.
-__global__ void __launch_bounds__(256)
-k_det_finish(const fmcw_det* __restrict__ scratch, uint32_t scratch_cap, const uint32_t* __restrict__ wg_base,
-             const uint32_t* __restrict__ wg_count, const uint32_t* __restrict__ wg_off,
-             const uint32_t* __restrict__ block_sum, int nb, int n, fmcw_det* __restrict__ out, uint32_t cap,
-             uint32_t* __restrict__ n_dets, uint32_t* __restrict__ counter, uint32_t* __restrict__ sat,
-             uint32_t* __restrict__ k3_ctr, int n_k3) {
-  __shared__ uint32_t s_red[2][4];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int jb = (int)((blockIdx.x * 256u) >> 10);  // this workgroup's level-1 block
-  uint32_t pre = 0, all = 0;
-  for (int j = threadIdx.x; j < nb; j += 256) {
-    const uint32_t v = block_sum[j];
-    pre += j < jb ? v : 0u;
-    all += v;
-  }
+// Look-back status word of workgroup w: high half = this call's epoch << 2 | error << 1 |
+// inclusive, low half = w's detection count (aggregate) or, once inclusive, the count of tiles
+// 0 .. kDetTiles (w + 1) - 1.  One 64-bit store / load at agent scope: coherent across the XCDs' L2s.
+constexpr uint32_t kLbIncl = 1u, kLbErr = 2u;
+#ifndef FMCW_DET_TILES
+#define FMCW_DET_TILES 1024
+#endif
+constexpr int kDetTiles = FMCW_DET_TILES;  // tiles (= threads) per k_det_list workgroup (256: lab A/B)
+constexpr uint32_t kLbMaxPolls = 1u << 20;  // >> any real wait (one poll ~1 us): a safety net only
+
+__device__ __forceinline__ void lb_publish(uint64_t* st, uint32_t hi, uint32_t v) {
+  __hip_atomic_store(st, ((uint64_t)hi << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Round 4: one launch instead of a level-1 scan launch plus a level-2 / copy launch.  Workgroup
+// w owns tiles kDetTiles w .. kDetTiles (w + 1) - 1, one per thread: it scans their counts, publishes its aggregate, and takes
+// its offset by decoupled look-back -- wave 0 reads the status words of the 64 nearest
+// predecessors at once and sums back to the nearest inclusive one.  A workgroup only waits for
+// lower ids, which the dispatcher started before it, so the chain drains; the wait is bounded
+// all the same, and a workgroup that gives up marks its word (and so every later one) with an
+// error the last workgroup reports as every detection lost.  One lane per tile copies the
+// tile's records; a tile with more than 8 (a target's row) is copied by the whole wave, 64
+// records per step, so one hot tile does not serialise the kernel.  The last workgroup writes
+// the status words -- [0] every detection found, [1] of which not stored, [2] / [3] the
+// saturation counts the call's K1 / K2 accumulated in the handle's `sat` -- and re-arms the
+// handle's per-call counters (overflow use, drops, saturations, the 2-D CFAR launches'
+// candidate counters) for the next call: every kernel that uses them ran before this one.
+__global__ void __launch_bounds__(kDetTiles)
+k_det_list(const fmcw_det* __restrict__ scratch, uint32_t scratch_cap, const uint32_t* __restrict__ wg_base,
+           const uint32_t* __restrict__ wg_count, int n, fmcw_det* __restrict__ out, uint32_t cap,
+           uint64_t* __restrict__ lb, uint32_t epoch, uint32_t* __restrict__ n_dets, uint32_t* __restrict__ counter,
+           uint32_t* __restrict__ sat, uint32_t* __restrict__ k3_ctr, int n_k3) {
+  __shared__ int s_wave[kDetTiles / 64 + 1];
+  __shared__ uint32_t s_pre, s_err;
+  const int lane = threadIdx.x & 63;
+  const int w = blockIdx.x;
+  const int i = w * kDetTiles + threadIdx.x;
+  const uint32_t c = i < n ? wg_count[i] : 0u;
+  int agg;
+  const uint32_t e = (uint32_t)block_excl_scan<kDetTiles>((int)c, s_wave, agg);
+  const uint32_t tag = epoch << 2;
+  if (threadIdx.x < 64) {
+    uint32_t pre = 0, err = 0;
+    if (w > 0) {
+      if (lane == 0) lb_publish(lb + w, tag, (uint32_t)agg);
+      int top = w - 1;  // nearest predecessor not yet summed
+      uint32_t polls = 0;
+      for (;;) {
+        const int k = top - lane;
+        uint32_t hi = tag | kLbIncl, v = 0;  // below workgroup 0: an inclusive zero
+        if (k >= 0) {
+          const uint64_t x = __hip_atomic_load(lb + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          hi = (uint32_t)(x >> 32);
+          v = (uint32_t)x;
+        }
+        const bool ready = (hi >> 2) == epoch;
+        const uint64_t rdy = __ballot(ready), inc = __ballot(ready && (hi & kLbIncl));
+        const int f = inc ? __builtin_ctzll(inc) : 63;            // nearest inclusive lane
+        const uint64_t need = f == 63 ? ~0ull : (2ull << f) - 1;  // lanes 0 .. f
+        if ((rdy & need) == need) {
+          uint32_t t = lane <= f ? v : 0u, te = lane <= f ? (hi & kLbErr) : 0u;
 #pragma unroll
-  for (int x = 32; x >= 1; x >>= 1) {
-    pre += (uint32_t)__shfl_xor((int)pre, x, 64);
-    all += (uint32_t)__shfl_xor((int)all, x, 64);
-  }
-  if (lane == 0) {
-    s_red[0][wv] = pre;
-    s_red[1][wv] = all;
-  }
-  __syncthreads();
-  const uint32_t P = s_red[0][0] + s_red[0][1] + s_red[0][2] + s_red[0][3];
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    n_dets[0] = s_red[1][0] + s_red[1][1] + s_red[1][2] + s_red[1][3];
-    n_dets[1] = counter[1];
-    n_dets[2] = sat ? sat[0] : 0u;
-    n_dets[3] = sat ? sat[1] : 0u;
-    counter[0] = 0u;
-    counter[1] = 0u;
-    if (sat) sat[0] = sat[1] = 0u;
-  }
-  if (blockIdx.x == 0)
-    for (int k = threadIdx.x; k < n_k3; k += 256) k3_ctr[k] = 0u;
-  if (!out) return;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  uint32_t c = 0, b = 0, o = 0;
-  if (i < n) {
-    c = wg_count[i];
-    if (c) {
-      b = wg_base[i];
-      o = P + wg_off[i];
+          for (int x = 32; x >= 1; x >>= 1) {
+            t += (uint32_t)__shfl_xor((int)t, x, 64);
+            te |= (uint32_t)__shfl_xor((int)te, x, 64);
+          }
+          pre += t;
+          err |= te;
+          if (inc) break;
+          top -= 64;
+          polls = 0;
+        } else if (++polls > kLbMaxPolls) {
+          err = kLbErr;
+          break;
+        }
+      }
+    }
+    if (lane == 0) {
+      lb_publish(lb + w, tag | kLbIncl | err, pre + (uint32_t)agg);
+      s_pre = pre;
+      s_err = err;
     }
   }
+  __syncthreads();
+  const uint32_t P = s_pre;
+  if (w == (int)gridDim.x - 1) {
+    if (threadIdx.x == 0) {
+      n_dets[0] = P + (uint32_t)agg;
+      n_dets[1] = s_err ? 0xffffffffu : counter[1];
+      n_dets[2] = sat ? sat[0] : 0u;
+      n_dets[3] = sat ? sat[1] : 0u;
+      counter[0] = 0u;
+      counter[1] = 0u;
+      if (sat) sat[0] = sat[1] = 0u;
+    }
+    for (int k = threadIdx.x; k < n_k3; k += kDetTiles) k3_ctr[k] = 0u;
+  }
+  if (!out) return;
+  const uint32_t b = c ? wg_base[i] : 0u, o = P + e;
   if (c <= 8)
     for (uint32_t k = 0; k < c; ++k)
       if (b + k < scratch_cap && o + k < cap) out[o + k] = scratch[b + k];
@@ -206,13 +236,13 @@ struct fmcw_handle {
   uint32_t* counter = nullptr;  // [0] overflow entries used, [1] dropped
   uint32_t* sat = nullptr;      // [0] window, [1] word saturations of the current call (status words 2, 3)
   // the per-call device counters (counter[0..1], sat, k3_ctr) are zero: re-armed by the previous
-  // call's k_det_finish (or at fmcw_create); a call that stopped early leaves this false and the
+  // call's k_det_list (or at fmcw_create); a call that stopped early leaves this false and the
   // next one zeroes them first
   bool counters_armed = false;
   uint32_t* wg_base = nullptr;
   uint32_t* wg_count = nullptr;
-  uint32_t* wg_off = nullptr;
-  uint32_t* block_sum = nullptr;  // ceil(n_wg_max / 1024) scan blocks
+  uint64_t* lb_status = nullptr;  // k_det_list look-back words, one per kDetTiles tiles
+  uint32_t det_epoch = 0;          // k_det_list's call tag (1 .. 2^30 - 1; the words start at 0)
   uint32_t* n_dets_tmp = nullptr;
   size_t n_wg_max = 0;
   // fmcw_process host-copy staging, grown on demand and kept (no allocator call per frame batch)
@@ -480,8 +510,8 @@ int cfar2_steps_model(int nf, int tpf, int grid, int tr, int hr) {
   return best;
 }
 
-// Zero the per-call counters unless the previous call's k_det_finish left them armed; the flag
-// drops until this call's k_det_finish is enqueued.
+// Zero the per-call counters unless the previous call's k_det_list left them armed; the flag
+// drops until this call's k_det_list is enqueued.
 int arm_counters(fmcw_handle* h, hipStream_t s) {
   if (!h->counters_armed) {
     hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(256), 0, s, h->counter, 2, h->sat, 2, h->k3_ctr,
@@ -544,18 +574,18 @@ int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipS
 int launch_det_finish(fmcw_handle* h, size_t n_frames, fmcw_det* dets, size_t det_cap,
                       uint32_t* n_dets_dev, uint32_t* sat, hipStream_t s) {
   const int n = (int)(n_frames * tiles_per_frame(h));
-  const int nb = (n + 1023) / 1024;
+  if (n < 1 || (size_t)n > h->n_wg_max) return fail(FMCW_EINVAL, "detection list over %d tiles", n);
+  h->det_epoch = (h->det_epoch + 1) & 0x3fffffffu;
+  if (!h->det_epoch) h->det_epoch = 1;
   ProfScope ps(h, FMCW_K_COMPACT);
-  launch_k(ps, false, k_det_scan_blocks, dim3(nb), dim3(1024), 0u, s, (const uint32_t*)h->wg_count, h->wg_off, n,
-           h->block_sum);
   // entries past the handle's scratch capacity are never stored: clip to it as well
   const bool copy = dets && det_cap;
   const uint32_t cap = copy ? (uint32_t)std::min<size_t>(det_cap, h->det_scratch_cap) : 0u;
-  launch_k(ps, true, k_det_finish, dim3(copy ? (n + 255) / 256 : 1), dim3(256), 0u, s,
-           (const fmcw_det*)h->det_scratch, h->det_scratch_cap, (const uint32_t*)h->wg_base,
-           (const uint32_t*)h->wg_count, (const uint32_t*)h->wg_off, (const uint32_t*)h->block_sum, nb, n,
-           copy ? dets : (fmcw_det*)nullptr, cap, n_dets_dev, h->counter, sat, h->k3_ctr, 2 * h->k3_launches);
-  return check_launch("k_det_scan_blocks / k_det_finish");
+  launch_k(ps, true, k_det_list, dim3((n + kDetTiles - 1) / kDetTiles), dim3(kDetTiles), 0u, s, (const fmcw_det*)h->det_scratch,
+           h->det_scratch_cap, (const uint32_t*)h->wg_base, (const uint32_t*)h->wg_count, n,
+           copy ? dets : (fmcw_det*)nullptr, cap, h->lb_status, h->det_epoch, n_dets_dev, h->counter, sat, h->k3_ctr,
+           2 * h->k3_launches);
+  return check_launch("k_det_list");
 }
 
 // 2^-range_shift for the Q15 window path (the fp32 window tables carry it otherwise)
@@ -750,8 +780,7 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   ALLOC(h->n_dets_tmp, 16);
   ALLOC(h->wg_base, h->n_wg_max * sizeof(uint32_t));
   ALLOC(h->wg_count, h->n_wg_max * sizeof(uint32_t));
-  ALLOC(h->wg_off, h->n_wg_max * sizeof(uint32_t));
-  ALLOC(h->block_sum, ((h->n_wg_max + 1023) / 1024 + 1) * sizeof(uint32_t));
+  ALLOC(h->lb_status, ((h->n_wg_max + kDetTiles - 1) / kDetTiles) * sizeof(uint64_t));
 #undef ALLOC
   {
     // the range table carries the 2^-range_shift scaling (Q15: applied after the integer window)
@@ -759,7 +788,8 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
                        wd = window_table(c.n_doppler, c.window);  // Q15: the ROM integers, applied by K2
     if (hipMemcpy(h->win_r, wr.data(), wr.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(h->win_d, wd.data(), wd.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemset(h->wg_count, 0, h->n_wg_max * sizeof(uint32_t)) != hipSuccess)
+        hipMemset(h->wg_count, 0, h->n_wg_max * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(h->lb_status, 0, ((h->n_wg_max + kDetTiles - 1) / kDetTiles) * sizeof(uint64_t)) != hipSuccess)
       return cleanup(fail(FMCW_EHIP, "window upload failed"));
   }
   if (c.cfar_kind == FMCW_CFAR_OS2D) {
@@ -792,7 +822,7 @@ int fmcw_destroy(fmcw_handle* h) {
   if (!h) return FMCW_OK;
   hipSetDevice(h->cfg.device_id);
   void* ptrs[] = {h->win_r, h->win_d, h->inter, h->lin_scratch, h->det_scratch, h->counter, h->sat,
-                  h->n_dets_tmp, h->wg_base, h->wg_count, h->wg_off, h->block_sum,
+                  h->n_dets_tmp, h->wg_base, h->wg_count, h->lb_status,
                   h->stage_cube, h->stage_map, h->stage_dets, h->cand_cell, h->cand_thr,
                   h->cand_tiles, h->k3_ctr};
   for (void* p : ptrs)
@@ -823,7 +853,7 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
   const Cfar1DArgs cf1 = cfar1_args(c);
   const bool q15 = c.window == FMCW_WIN_Q15_RTL;
   // status words 2 / 3 (saturations) are counted atomically by the kernels that can saturate: into
-  // the handle's `sat` words, which the call's last kernel (k_det_finish) reports and re-arms
+  // the handle's `sat` words, which the call's last kernel (k_det_list) reports and re-arms
   // with the other per-call counters; without a CFAR there is no such kernel, and the caller's
   // words are zeroed and counted into directly
   const bool cfar = c.cfar_kind != FMCW_CFAR_NONE;
@@ -885,7 +915,7 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
   }
   if (cfar) {
     if ((rc = launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, h->sat, s))) return rc;
-    h->counters_armed = true;  // k_det_finish re-arms them on the device, in stream order
+    h->counters_armed = true;  // k_det_list re-arms them on the device, in stream order
   }
   return FMCW_OK;
 }

@@ -4,7 +4,7 @@
 //  K2 k_doppler   Doppler window + FFT + |X| / NCI + map + 1-D OS-CFAR, one wave per tile
 //                                                        (radar_core.vhd:340-374, os_cfar.vhd)
 //  K3 k_cfar2d    2-D OS-CFAR over the magnitude map       (os_cfar_2d.vhd:83-230)
-//     k_det_scan_blocks / k_det_finish   deterministic detection list (radar_core.vhd:396-418)
+//     k_det_list (fmcw_api.hip)          deterministic detection list (radar_core.vhd:396-418)
 //
 // Intermediate (corner-turned range spectrum) layout in HBM, per (frame, rx):
 //     inter[rb][cb][RB][T]  complex fp32,  rb = r / RB, cb = c / T
@@ -662,7 +662,7 @@ k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const floa
 // slot_cap detections reserves room in the overflow region with one atomic (a single global
 // counter serialises at ~88 returning atomics/us, MI355X_MICROARCH "dequeue", which is why
 // the common path must not touch it).  (wg_base, wg_count) per tile then let
-// k_det_scan_blocks / k_det_finish order the list by tile id = (frame, range): deterministic.
+// k_det_list order the list by tile id = (frame, range): deterministic.
 // Detections that fit nowhere are counted in counter[1] (reported as FMCW_EDETCAP).
 // --------------------------------------------------------------------------------------
 struct DetSink {

@@ -224,7 +224,9 @@ int fmcw_destroy(fmcw_handle* h);
  *   [0] detections found (may exceed det_cap; entries beyond det_cap are not written),
  *   [1] detections lost because the handle's internal detection scratch overflowed (a tile
  *       with more than its slot that also found the shared overflow region full).  Non-zero
- *       means the list is incomplete; fmcw_process returns FMCW_EDETCAP then,
+ *       means the list is incomplete; fmcw_process returns FMCW_EDETCAP then.  0xffffffff:
+ *       the ordering pass could not complete (a safety net that bounds its wait; not expected),
+ *       the whole list is void,
  *   [2] samples saturated by the RTL-compat integer windows (FMCW_WIN_Q15_RTL, either axis;
  *       win1 / win2 saturation_flag, window_multiplier.vhd:152-158),
  *   [3] samples whose int16 spectrum word or canceller output was clipped (FMCW_COMPAT_MTI or

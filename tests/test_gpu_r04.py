@@ -99,7 +99,7 @@ def test_cfar2d_dense_candidates_exact_count():
 
 def test_counters_rearmed_across_calls():
     """The per-call device counters (overflow use, drops, saturations, the 2-D CFAR launches'
-    candidate counters) are re-armed by each call's last kernel (k_det_finish), not zeroed at the
+    candidate counters) are re-armed by each call's last kernel (k_det_list), not zeroed at the
     next call's start: alternate fmcw_cfar stage calls on a map that fills the overflow region
     (every third cell detects) with whole-path calls on a cube, on one handle, and check every
     call against the oracle."""
