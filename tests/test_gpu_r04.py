@@ -116,3 +116,26 @@ def test_counters_rearmed_across_calls():
             out = core.process(cube)
             np.testing.assert_array_equal(out.dets, CB.cfar(out.rd_map, O.Cfar2D(), threads=16))
             assert out.n_dets >= nf and out.window_saturations == 0 and out.word_saturations == 0
+
+
+def test_detection_list_many_blocks():
+    """The one-pass ordered list (k_det_list, decoupled look-back over 1024-tile blocks) at config
+    2's bench shape -- 1024 frames in one call, ten K1 -> K2 chunks, far more than 64 look-back
+    blocks, so a workgroup may sum several windows of predecessors -- equals the same frames run as
+    16 calls of 64 frames (a few blocks each), frame ids shifted; two whole calls agree (the
+    look-back words are reused under the next call's epoch)."""
+    ns, nc, F, part = 1024, 256, 1024, 64
+    base = synth.frames(part, ns, nc, 1, "two_targets", seed=61, dtype="i16")
+    cube = np.concatenate([base] * (F // part))
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os1d", in_dtype="i16", max_frames=F) as core:
+        whole = core.process(cube, want_map=False)
+        again = core.process(cube, want_map=False)
+        parts = [core.process(cube[k * part:(k + 1) * part], want_map=False) for k in range(F // part)]
+    np.testing.assert_array_equal(whole.dets, again.dets)
+    cat = []
+    for k, p in enumerate(parts):
+        d = p.dets.copy()
+        d["frame"] += k * part
+        cat.append(d)
+    np.testing.assert_array_equal(whole.dets, np.concatenate(cat))
+    assert whole.n_dets == sum(p.n_dets for p in parts) >= F
