@@ -523,8 +523,14 @@ int arm_counters(fmcw_handle* h, hipStream_t s) {
 }
 
 constexpr size_t kCfar2Batch = 16;  // frames per 2-D CFAR launch on the caller's map (at least)
-constexpr int kCfar2DecideGrid = 1024;  // K3b workgroups (4 waves each, one candidate per wave at a time)
-constexpr int kCfar2EmitGrid = 256;     // K3c workgroups (one wave tile per wave at a time)
+#ifndef FMCW_K3_DECIDE_GRID
+#define FMCW_K3_DECIDE_GRID 1024
+#endif
+#ifndef FMCW_K3_EMIT_GRID
+#define FMCW_K3_EMIT_GRID 256
+#endif
+constexpr int kCfar2DecideGrid = FMCW_K3_DECIDE_GRID;  // K3b workgroups (4 waves each, one candidate per wave at a time)
+constexpr int kCfar2EmitGrid = FMCW_K3_EMIT_GRID;      // K3c workgroups (one wave tile per wave at a time)
 
 // The CFAR launcher shared by fmcw_enqueue (map just produced by K2) and fmcw_cfar.
 int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipStream_t s) {
