@@ -42,6 +42,11 @@ __global__ void k_zero_words(uint32_t* __restrict__ a, int na, uint32_t* __restr
 // Look-back status word of workgroup w: high half = this call's epoch << 2 | error << 1 |
 // inclusive, low half = w's detection count (aggregate) or, once inclusive, the count of tiles
 // 0 .. kDetTiles (w + 1) - 1.  One 64-bit store / load at agent scope: coherent across the XCDs' L2s.
+// The epoch lives in device memory (ep[0], 1 .. 2^30 - 1; ep[1] counts the workgroups that have
+// published their inclusive word): every workgroup reads it once at its start, and the last one
+// to publish -- when every workgroup of the launch has read it -- advances it and re-arms ep[1].
+// So a launch captured into a hipGraph tags its words afresh on every replay (a host-chosen epoch
+// would be baked into the graph, and a replay could take a previous replay's word for its own).
 constexpr uint32_t kLbIncl = 1u, kLbErr = 2u;
 #ifndef FMCW_DET_TILES
 #define FMCW_DET_TILES 1024
@@ -69,8 +74,8 @@ __device__ __forceinline__ void lb_publish(uint64_t* st, uint32_t hi, uint32_t v
 __global__ void __launch_bounds__(kDetTiles)
 k_det_list(const fmcw_det* __restrict__ scratch, uint32_t scratch_cap, const uint32_t* __restrict__ wg_base,
            const uint32_t* __restrict__ wg_count, int n, fmcw_det* __restrict__ out, uint32_t cap,
-           uint64_t* __restrict__ lb, uint32_t epoch, uint32_t* __restrict__ n_dets, uint32_t* __restrict__ counter,
-           uint32_t* __restrict__ sat, uint32_t* __restrict__ k3_ctr, int n_k3) {
+           uint64_t* __restrict__ lb, uint32_t* __restrict__ ep, uint32_t* __restrict__ n_dets,
+           uint32_t* __restrict__ counter, uint32_t* __restrict__ sat, uint32_t* __restrict__ k3_ctr, int n_k3) {
   __shared__ int s_wave[kDetTiles / 64 + 1];
   __shared__ uint32_t s_pre, s_err;
   const int lane = threadIdx.x & 63;
@@ -79,8 +84,11 @@ k_det_list(const fmcw_det* __restrict__ scratch, uint32_t scratch_cap, const uin
   const uint32_t c = i < n ? wg_count[i] : 0u;
   int agg;
   const uint32_t e = (uint32_t)block_excl_scan<kDetTiles>((int)c, s_wave, agg);
-  const uint32_t tag = epoch << 2;
   if (threadIdx.x < 64) {
+    // this launch's epoch (set by the previous launch's last publisher: visible at launch start)
+    const uint32_t epoch = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const uint32_t tag = epoch << 2;
     uint32_t pre = 0, err = 0;
     if (w > 0) {
       if (lane == 0) lb_publish(lb + w, tag, (uint32_t)agg);
@@ -120,6 +128,13 @@ k_det_list(const fmcw_det* __restrict__ scratch, uint32_t scratch_cap, const uin
       lb_publish(lb + w, tag | kLbIncl | err, pre + (uint32_t)agg);
       s_pre = pre;
       s_err = err;
+      // the last workgroup to get here: every other one has read `epoch` (it did so before
+      // publishing), so the next launch's epoch can be set, and the count re-armed
+      if (__hip_atomic_fetch_add(ep + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+        const uint32_t nx = (epoch + 1u) & 0x3fffffffu;
+        __hip_atomic_store(ep + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ep, nx ? nx : 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
   __syncthreads();
@@ -242,7 +257,7 @@ struct fmcw_handle {
   uint32_t* wg_base = nullptr;
   uint32_t* wg_count = nullptr;
   uint64_t* lb_status = nullptr;  // k_det_list look-back words, one per kDetTiles tiles
-  uint32_t det_epoch = 0;          // k_det_list's call tag (1 .. 2^30 - 1; the words start at 0)
+  uint32_t* det_epoch = nullptr;   // k_det_list's device-resident call tag and publish count (2 words)
   uint32_t* n_dets_tmp = nullptr;
   size_t n_wg_max = 0;
   // fmcw_process host-copy staging, grown on demand and kept (no allocator call per frame batch)
@@ -510,15 +525,27 @@ int cfar2_steps_model(int nf, int tpf, int grid, int tr, int hr) {
   return best;
 }
 
+// true while `s` is being captured into a hipGraph (nothing the call enqueues runs now)
+bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return st == hipStreamCaptureStatusActive;
+}
+
 // Zero the per-call counters unless the previous call's k_det_list left them armed; the flag
-// drops until this call's k_det_list is enqueued.
-int arm_counters(fmcw_handle* h, hipStream_t s) {
-  if (!h->counters_armed) {
+// drops until this call's k_det_list is enqueued.  A call captured into a graph always zeroes
+// them (a replay may follow any call, including one that stopped early) and leaves the flag as
+// it was: capturing runs nothing, so the device state is still the one the flag describes.
+int arm_counters(fmcw_handle* h, hipStream_t s, bool cap) {
+  if (!h->counters_armed || cap) {
     hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(256), 0, s, h->counter, 2, h->sat, 2, h->k3_ctr,
                        2 * h->k3_launches);
     if (int rc = check_launch("k_zero_words")) return rc;
   }
-  h->counters_armed = false;
+  if (!cap) h->counters_armed = false;
   return FMCW_OK;
 }
 
@@ -581,8 +608,6 @@ int launch_det_finish(fmcw_handle* h, size_t n_frames, fmcw_det* dets, size_t de
                       uint32_t* n_dets_dev, uint32_t* sat, hipStream_t s) {
   const int n = (int)(n_frames * tiles_per_frame(h));
   if (n < 1 || (size_t)n > h->n_wg_max) return fail(FMCW_EINVAL, "detection list over %d tiles", n);
-  h->det_epoch = (h->det_epoch + 1) & 0x3fffffffu;
-  if (!h->det_epoch) h->det_epoch = 1;
   ProfScope ps(h, FMCW_K_COMPACT);
   // entries past the handle's scratch capacity are never stored: clip to it as well
   const bool copy = dets && det_cap;
@@ -752,10 +777,15 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   if (c.cfar_kind == FMCW_CFAR_OS2D) {
     ALLOC(h->lin_scratch, (size_t)h->chunk * c.n_range * c.n_doppler * sizeof(float));
     // candidate lists for K3 launches of up to k3_frames frames (fmcw_enqueue's batches: >= 16
-    // frames, ending on a chunk boundary): every cell may be a candidate, so they cannot overflow
-    h->k3_frames = (int)std::min<size_t>(c.max_frames, kCfar2Batch + h->chunk);
-    const size_t cells = (size_t)h->k3_frames * c.n_range * c.n_doppler;
-    if (cells > 0xffffffffu) return cleanup(fail(FMCW_EINVAL, "2-D CFAR launch too large for 32-bit cell indices"));
+    // frames, ending on a chunk boundary, so at most 16 + chunk - 1
+    // frames): every cell may be a candidate, so they cannot overflow.  8 B per cell: at 8192 x
+    // 1024 with the auto chunk (3 frames) 19 frames, 1.2 GiB.  A K3 launch addresses its cells with
+    // 32-bit indices, so k3_frames is also capped at 2^32 cells (launch_cfar splits longer
+    // batches into pieces of k3_frames).
+    const size_t frame_cells = (size_t)c.n_range * c.n_doppler;
+    h->k3_frames = (int)std::max<size_t>(1, std::min<size_t>({(size_t)c.max_frames, kCfar2Batch + h->chunk,
+                                                              (size_t)0xffffffffu / frame_cells}));
+    const size_t cells = (size_t)h->k3_frames * frame_cells;
     // K3 launches per call: one per chunk at most (map-less calls run it on each chunk's scratch),
     // else one per >= 16-frame batch, or one per k3_frames piece (fmcw_cfar)
     const size_t minb = std::min<size_t>(h->chunk, kCfar2Batch);
@@ -787,15 +817,18 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   ALLOC(h->wg_base, h->n_wg_max * sizeof(uint32_t));
   ALLOC(h->wg_count, h->n_wg_max * sizeof(uint32_t));
   ALLOC(h->lb_status, ((h->n_wg_max + kDetTiles - 1) / kDetTiles) * sizeof(uint64_t));
+  ALLOC(h->det_epoch, 2 * sizeof(uint32_t));
 #undef ALLOC
   {
+    static const uint32_t kEpoch0[2] = {1u, 0u};  // first epoch 1 (the look-back words start at 0)
     // the range table carries the 2^-range_shift scaling (Q15: applied after the integer window)
     std::vector<float> wr = window_table(c.n_range, c.window, c.window == FMCW_WIN_Q15_RTL ? 0 : c.range_shift),
                        wd = window_table(c.n_doppler, c.window);  // Q15: the ROM integers, applied by K2
     if (hipMemcpy(h->win_r, wr.data(), wr.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(h->win_d, wd.data(), wd.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(h->wg_count, 0, h->n_wg_max * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(h->lb_status, 0, ((h->n_wg_max + kDetTiles - 1) / kDetTiles) * sizeof(uint64_t)) != hipSuccess)
+        hipMemset(h->lb_status, 0, ((h->n_wg_max + kDetTiles - 1) / kDetTiles) * sizeof(uint64_t)) != hipSuccess ||
+        hipMemcpy(h->det_epoch, kEpoch0, sizeof kEpoch0, hipMemcpyHostToDevice) != hipSuccess)
       return cleanup(fail(FMCW_EHIP, "window upload failed"));
   }
   if (c.cfar_kind == FMCW_CFAR_OS2D) {
@@ -828,7 +861,7 @@ int fmcw_destroy(fmcw_handle* h) {
   if (!h) return FMCW_OK;
   hipSetDevice(h->cfg.device_id);
   void* ptrs[] = {h->win_r, h->win_d, h->inter, h->lin_scratch, h->det_scratch, h->counter, h->sat,
-                  h->n_dets_tmp, h->wg_base, h->wg_count, h->lb_status,
+                  h->n_dets_tmp, h->wg_base, h->wg_count, h->lb_status, h->det_epoch,
                   h->stage_cube, h->stage_map, h->stage_dets, h->cand_cell, h->cand_thr,
                   h->cand_tiles, h->k3_ctr};
   for (void* p : ptrs)
@@ -869,7 +902,9 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
     hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(256), 0, s, nullptr, 0, n_dets_dev, FMCW_STATUS_WORDS, nullptr, 0);
     if ((rc = check_launch("k_zero_words"))) return rc;
   }
-  if (cfar && (rc = arm_counters(h, s))) return rc;
+  const bool cap = capturing(s);
+  if (cap && h->profiling) return fail(FMCW_EINVAL, "profiling events cannot be captured into a graph");
+  if (cfar && (rc = arm_counters(h, s, cap))) return rc;
   h->k3_launch_idx = 0;
 
   // Chunks of h->chunk frames: K1 -> corner-turned spectrum -> K2 (+ K3)
@@ -921,7 +956,7 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
   }
   if (cfar) {
     if ((rc = launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, h->sat, s))) return rc;
-    h->counters_armed = true;  // k_det_list re-arms them on the device, in stream order
+    if (!cap) h->counters_armed = true;  // k_det_list re-arms them on the device, in stream order
   }
   return FMCW_OK;
 }
@@ -1026,12 +1061,14 @@ int fmcw_cfar(fmcw_handle* h, const float* map, size_t n_frames, fmcw_det* dets,
   if (n_frames < 1 || n_frames > c.max_frames) return fail(FMCW_EINVAL, "n_frames out of range");
   HIP_TRY(hipSetDevice(c.device_id));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (int rc0 = arm_counters(h, s)) return rc0;
+  const bool cap = capturing(s);
+  if (cap && h->profiling) return fail(FMCW_EINVAL, "profiling events cannot be captured into a graph");
+  if (int rc0 = arm_counters(h, s, cap)) return rc0;
   h->k3_launch_idx = 0;
   int rc = launch_cfar(h, map, (int)n_frames, 0, s);
   if (rc) return rc;
   if ((rc = launch_det_finish(h, n_frames, dets, det_cap, n_dets_dev, nullptr, s))) return rc;
-  h->counters_armed = true;
+  if (!cap) h->counters_armed = true;
   return FMCW_OK;
 }
 

@@ -18,6 +18,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 
 #include "../../include/fmcw.h"
 
@@ -92,6 +93,25 @@ __global__ void __launch_bounds__(256) k_gather_compact(const fmcw_det* __restri
   }
 }
 
+// fmcw_comm_create's collective check: 3 words, all-reduced with max over the ranks (wire_cap,
+// ~wire_cap, any rank's allocation failure).  A static device array, so that no rank can fail to
+// obtain it and skip the collective its peers wait in.
+__device__ uint64_t g_check[3];
+std::mutex g_check_mu;
+bool g_fail_next_alloc = false;  // fmcw_comm_fail_next_alloc_for_test
+
+// The verdict of the check, the same on every rank: the all-reduced words h (or this rank's own,
+// n_ranks == 1) against this rank's wire_cap and allocation result.
+int comm_check_decide(const uint64_t (&h)[3], bool local_fail, size_t wire_cap, size_t msg) {
+  if (h[2])
+    return local_fail ? gfail(FMCW_ENOMEM, "gather buffers (%zu B per rank) failed", msg)
+                      : gfail(FMCW_ENOMEM, "gather buffers failed on another rank");
+  if (h[0] != wire_cap || ~h[1] != wire_cap)
+    return gfail(FMCW_EINVAL, "wire_cap differs between ranks (this rank %zu, max %llu, min %llu)", wire_cap,
+                 (unsigned long long)h[0], (unsigned long long)~h[1]);
+  return FMCW_OK;
+}
+
 }  // namespace
 
 struct fmcw_comm {
@@ -137,51 +157,53 @@ int fmcw_comm_create(const void* id, int n_ranks, int rank, int device_id, size_
     return gfail(FMCW_EHIP, "ncclCommInitRank: %s", ncclGetErrorString(r));
   }
   const size_t msg = (1 + wire_cap) * sizeof(fmcw_det);
-  // the check word of the collective below first: it is tiny, and a rank that cannot even get it
-  // aborts the communicator, so the other ranks' all-reduce fails instead of waiting for it
-  uint64_t* v = nullptr;
-  if (n_ranks > 1 && hipMalloc(reinterpret_cast<void**>(&v), 3 * sizeof(uint64_t)) != hipSuccess) {
-    (void)hipGetLastError();
-    ncclCommAbort(c->comm);
-    c->comm = nullptr;
-    fmcw_comm_destroy(c);
-    return gfail(FMCW_ENOMEM, "gather check word: hipMalloc failed (communicator aborted)");
-  }
-  // a failed buffer allocation is not returned at once: every rank still joins the all-reduce
-  // (with a failure flag), so a local failure fails the whole job instead of hanging the others
-  bool local_fail = false;
-  if (hipMalloc(reinterpret_cast<void**>(&c->wire), msg) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&c->recv), msg * (size_t)n_ranks) != hipSuccess) {
+  // A failed buffer allocation is not returned at once: every rank still joins the one all-reduce
+  // below (with a failure flag), so a local failure fails the whole job instead of hanging the
+  // other ranks in their all-reduce.  Nothing before that collective can fail alone: the check
+  // words are a static device array (no allocation), and the allocations only set the flag.
+  bool local_fail = g_fail_next_alloc;
+  g_fail_next_alloc = false;
+  if (!local_fail && (hipMalloc(reinterpret_cast<void**>(&c->wire), msg) != hipSuccess ||
+                      hipMalloc(reinterpret_cast<void**>(&c->recv), msg * (size_t)n_ranks) != hipSuccess)) {
     (void)hipGetLastError();
     local_fail = true;
   }
+  uint64_t h[3] = {(uint64_t)wire_cap, ~(uint64_t)wire_cap, local_fail ? 1u : 0u};  // max: max, ~min, any failed
   if (n_ranks > 1) {
     // every rank must size its message alike (send / recv sizes match) and have its buffers: one
     // collective check here, the only host synchronisation of the communicator's life
-    uint64_t h[3] = {(uint64_t)wire_cap, ~(uint64_t)wire_cap, local_fail ? 1u : 0u};  // max: max, ~min, any failed
+    std::lock_guard<std::mutex> lk(g_check_mu);  // one static check array per device and process
+    void* v = nullptr;
     ncclResult_t rr = ncclSuccess;
-    const bool ok = hipMemcpy(v, h, sizeof h, hipMemcpyHostToDevice) == hipSuccess &&
-                    (rr = ncclAllReduce(v, v, 3, ncclUint64, ncclMax, c->comm, nullptr)) == ncclSuccess &&
-                    hipMemcpy(h, v, sizeof h, hipMemcpyDeviceToHost) == hipSuccess;
-    hipFree(v);
+    bool ok = hipGetSymbolAddress(&v, HIP_SYMBOL(g_check)) == hipSuccess;
+    if (!ok) {
+      // no check word: abort the communicator so that the peers' all-reduce fails rather than waits
+      (void)hipGetLastError();
+      ncclCommAbort(c->comm);
+      c->comm = nullptr;
+      fmcw_comm_destroy(c);
+      return gfail(FMCW_EHIP, "gather check word: hipGetSymbolAddress failed (communicator aborted)");
+    }
+    ok = hipMemcpy(v, h, sizeof h, hipMemcpyHostToDevice) == hipSuccess;
+    if (!ok) {  // the same: never leave the peers waiting in the collective
+      (void)hipGetLastError();
+      ncclCommAbort(c->comm);
+      c->comm = nullptr;
+      fmcw_comm_destroy(c);
+      return gfail(FMCW_EHIP, "gather check word: upload failed (communicator aborted)");
+    }
+    ok = (rr = ncclAllReduce(v, v, 3, ncclUint64, ncclMax, c->comm, nullptr)) == ncclSuccess &&
+         hipMemcpy(h, v, sizeof h, hipMemcpyDeviceToHost) == hipSuccess;
     if (!ok) {
       (void)hipGetLastError();
       fmcw_comm_destroy(c);
       return gfail(FMCW_EHIP, "gather check (all-reduce): %s", ncclGetErrorString(rr));
     }
-    if (h[2]) {
-      fmcw_comm_destroy(c);
-      return local_fail ? gfail(FMCW_ENOMEM, "gather buffers (%zu B per rank) failed", msg)
-                        : gfail(FMCW_ENOMEM, "gather buffers failed on another rank");
-    }
-    if (h[0] != wire_cap || ~h[1] != wire_cap) {
-      fmcw_comm_destroy(c);
-      return gfail(FMCW_EINVAL, "wire_cap differs between ranks (this rank %zu, max %llu, min %llu)", wire_cap,
-                   (unsigned long long)h[0], (unsigned long long)~h[1]);
-    }
-  } else if (local_fail) {
+  }
+  const int rc = comm_check_decide(h, local_fail, wire_cap, msg);
+  if (rc != FMCW_OK) {
     fmcw_comm_destroy(c);
-    return gfail(FMCW_ENOMEM, "gather buffers (%zu B per rank) failed", msg);
+    return rc;
   }
   *out = c;
   return FMCW_OK;
@@ -235,6 +257,22 @@ int fmcw_gather_dets(fmcw_comm* c, const fmcw_det* dets_dev, size_t det_cap, con
     if (hipGetLastError() != hipSuccess) return gfail(FMCW_EHIP, "k_gather_compact launch");
   }
   return FMCW_OK;
+}
+
+// Test hooks of fmcw_comm_create's failure handling.  fail_next_alloc: the calling process's next
+// fmcw_comm_create takes its buffer allocation as failed (after ncclCommInitRank, before the
+// collective check).  check_decide: the check's verdict on all-reduced words `h` (max over the
+// ranks of {wire_cap, ~wire_cap, failed}), so a CPU-side multi-rank test can all-reduce the words
+// with another backend and see every rank return the same error.
+int fmcw_comm_fail_next_alloc_for_test(int enable) {
+  g_fail_next_alloc = enable != 0;
+  return FMCW_OK;
+}
+
+int fmcw_comm_check_decide_for_test(const uint64_t* h, int local_fail, size_t wire_cap) {
+  if (!h) return gfail(FMCW_EINVAL, "null argument");
+  const uint64_t w[3] = {h[0], h[1], h[2]};
+  return comm_check_decide(w, local_fail != 0, wire_cap, (1 + wire_cap) * sizeof(fmcw_det));
 }
 
 // Single-process test hooks: the pack and compaction kernels without RCCL, so one GPU can check

@@ -100,6 +100,8 @@ SIGNATURES = {
     "fmcw_comm_create": (_I, [_VP, _I, _I, _I, _SZ, C.POINTER(_VP)]),
     "fmcw_comm_destroy": (_I, [_VP]),
     "fmcw_gather_dets": (_I, [_VP, _VP, _SZ, _VP, C.c_uint32, _VP, _VP, _I, _VP]),
+    "fmcw_comm_fail_next_alloc_for_test": (_I, [_I]),
+    "fmcw_comm_check_decide_for_test": (_I, [C.POINTER(C.c_uint64), _I, _SZ]),
     "fmcw_gather_pack_for_test": (_I, [_VP, _SZ, _VP, _SZ, C.c_uint32, _VP, _VP]),
     "fmcw_gather_compact_for_test": (_I, [_VP, _I, _SZ, _VP, _VP, _VP]),
     "fmcw_tws_config_default": (None, [C.POINTER(FmcwTwsConfig)]),

@@ -32,7 +32,12 @@
  *   - Return value: 0 (FMCW_OK) or a negative fmcw_status.  fmcw_last_error() returns a
  *     thread-local message for the last failure on the calling thread.
  *   - fmcw_enqueue and the stage functions take DEVICE pointers only, are stream-ordered
- *     and asynchronous (nothing synchronises, nothing allocates: graph-capturable).
+ *     and asynchronous (nothing synchronises, nothing allocates).  fmcw_enqueue and fmcw_cfar
+ *     can be captured into a hipGraph (stream capture) and the graph replayed any number of
+ *     times, interleaved with direct calls on the same handle: the detection ordering pass keeps
+ *     its call tag in device memory, and a captured call always re-zeroes the per-call counters
+ *     first.  Replays of one handle's graphs must not overlap each other or other calls (one
+ *     stream at a time, below); profiling (fmcw_set_profiling) must be off while capturing.
  *   - fmcw_process accepts host or device pointers (detected with hipPointerGetAttributes),
  *     and returns after the results are in the caller's buffers.
  *   - A handle is not thread-safe: one handle per host thread, and one stream at a time
@@ -56,7 +61,7 @@
 extern "C" {
 #endif
 
-#define FMCW_ABI_VERSION 6  /* 2: fmcw_config grew compat_rtl, range_shift (27 words, 108 B);
+#define FMCW_ABI_VERSION 7  /* 2: fmcw_config grew compat_rtl, range_shift (27 words, 108 B);
                                3: + spectrum_dtype (28 words, 112 B);
                                4: FMCW_K_COUNT 5 -> 6, FMCW_INFO_PAIR_CHUNK;
                                5: n_dets_dev holds FMCW_STATUS_WORDS (4) words (saturation
@@ -66,7 +71,10 @@ extern "C" {
                                   fmcw_comm_create takes wire_cap, fmcw_gather_dets det_cap;
                                6: fmcw_set_param (FMCW_PARAM_CFAR2D_STEPS), FMCW_INFO_CFAR2D_STEPS;
                                   range-kernel id 1 (k_range2) retired; the library reads no
-                                  environment variable */
+                                  environment variable;
+                               7: fmcw_enqueue / fmcw_cfar graph-capturable (device-resident
+                                  ordering tag); fmcw_comm_fail_next_alloc_for_test,
+                                  fmcw_comm_check_decide_for_test */
 
 typedef enum {
   FMCW_OK = 0,
@@ -128,8 +136,13 @@ typedef struct fmcw_config {
   /* resources */
   uint32_t max_frames;     /* largest n_frames per call (scratch is sized for it) */
   uint32_t chunk_frames;   /* frames per internal kernel chunk (0 = auto: a chunk's corner-turned
-                            * spectrum within ~192 MiB of the 256 MiB Infinity Cache, rounded to
-                            * whole rounds of the persistent grids; 96 frames at 1024 x 256) */
+                            * spectrum within 208 MiB of the 256 MiB Infinity Cache, no rounding;
+                            * 104 frames at 1024 x 256 fp32, 3 at 4096 x 512 x 4 rx or 8192 x 1024).
+                            * Device memory of a handle: the chunk's spectrum (8 B per point), a
+                            * detection scratch of ~1/32 + 1/64 of max_frames' cells (16 B each),
+                            * and with the 2-D CFAR a chunk-sized linear map (4 B per cell) and
+                            * candidate lists of 8 B per cell for min(max_frames, 16 + chunk,
+                            * 2^32 cells) frames -- 1.2 GiB at 8192 x 1024 with the auto chunk */
   int32_t device_id;       /* HIP device ordinal */
   /* RTL-compat arithmetic, a bitmask of fmcw_compat; 0 = the fp32 build spec */
   uint32_t compat_rtl;
@@ -219,8 +232,10 @@ int fmcw_destroy(fmcw_handle* h);
 
 /* Full hot path on n_frames frames, device pointers, asynchronous on `stream`
  * (hipStream_t; NULL = default stream).  rd_map may be NULL.  dets may be NULL when
- * cfar_kind == NONE.  n_dets_dev points at FMCW_STATUS_WORDS device uint32 words, zeroed and
- * rewritten by every call (it may be NULL only when cfar_kind == NONE; then no status):
+ * cfar_kind == NONE.  n_dets_dev points at FMCW_STATUS_WORDS device uint32 words, written by
+ * the last kernel of every call that returns FMCW_OK (a call that returns an error may have
+ * left them as the previous call wrote them); it may be NULL only when cfar_kind == NONE (then
+ * no status):
  *   [0] detections found (may exceed det_cap; entries beyond det_cap are not written),
  *   [1] detections lost because the handle's internal detection scratch overflowed (a tile
  *       with more than its slot that also found the shared overflow region full).  Non-zero
@@ -271,6 +286,13 @@ int fmcw_comm_destroy(fmcw_comm* c);
 int fmcw_gather_dets(fmcw_comm* c, const fmcw_det* dets_dev, size_t det_cap,
                      const uint32_t* n_dets_dev, uint32_t frame_offset, fmcw_det* out_dev,
                      uint32_t* out_n_dev, int root, void* stream);
+/* Test hooks of fmcw_comm_create's failure handling: fail_next_alloc makes the process's next
+ * fmcw_comm_create treat its buffer allocation as failed (after ncclCommInitRank, before the
+ * collective check, which every rank joins whatever failed locally); check_decide returns that
+ * check's verdict on the all-reduced words h[3] = max over ranks of {wire_cap, ~wire_cap, failed}
+ * (FMCW_ENOMEM if any rank failed, FMCW_EINVAL if wire_cap differs, else FMCW_OK). */
+int fmcw_comm_fail_next_alloc_for_test(int enable);
+int fmcw_comm_check_decide_for_test(const uint64_t* h, int local_fail, size_t wire_cap);
 /* Single-GPU test hooks of the gather's device side (no RCCL): the rank-local pack into one
  * message of (1 + wire_cap) records, and the root's compaction of n_ranks such messages laid
  * end to end in msgs_dev. */

@@ -24,7 +24,7 @@ def test_header_and_binding_agree():
 
 def test_header_enums_match_binding():
     """Kernel ids, info keys and the status word count: the ctypes constants are the header's
-    (ABI 6: FMCW_K_COUNT = 4 entries from fmcw_kernel_times, 4 status words in n_dets_dev,
+    (ABI 6-7: FMCW_K_COUNT = 4 entries from fmcw_kernel_times, 4 status words in n_dets_dev,
     fmcw_set_param keys)."""
     src = L.HEADER_PATH.read_text()
     enum = {k: int(v) for k, v in re.findall(r"\b(FMCW_(?:K|INFO|PARAM)_[A-Z0-9_]+)\s*=\s*(\d+)", src)}
@@ -38,7 +38,7 @@ def test_header_enums_match_binding():
     assert enum["FMCW_INFO_WORD_SATURATIONS"] == L.INFO_WORD_SATURATIONS
     assert enum["FMCW_INFO_CFAR2D_STEPS"] == L.INFO_CFAR2D_STEPS
     assert enum["FMCW_PARAM_CFAR2D_STEPS"] == L.PARAM_CFAR2D_STEPS
-    assert re.search(r"#define FMCW_ABI_VERSION 6\b", src)
+    assert re.search(r"#define FMCW_ABI_VERSION 7\b", src)
     assert int(re.search(r"#define FMCW_STATUS_WORDS (\d+)", src).group(1)) == L.STATUS_WORDS
 
 
@@ -63,7 +63,7 @@ def test_gfx950_code_object_present(lib_built):
 
 def test_struct_layouts():
     assert C.sizeof(L.FmcwDet) == 16
-    assert C.sizeof(L.FmcwConfig) == 28 * 4          # ABI 3-6 (fmcw.h FMCW_ABI_VERSION)
+    assert C.sizeof(L.FmcwConfig) == 28 * 4          # ABI 3-7 (fmcw.h FMCW_ABI_VERSION)
     assert L.FmcwDet.range.offset == 4 and L.FmcwDet.mag.offset == 8
 
 
@@ -77,7 +77,7 @@ def test_defaults_mirror_radar_core(lib_built):
             cfg.cfar2d_scale_max, cfg.cfar2d_scale_override) == (75, 2, 4, 6, 0)
     assert (cfg.cfar1d_ref, cfg.cfar1d_guard, cfg.cfar1d_rank) == (8, 2, 12)
     assert cfg.cfar1d_alpha == 4.0
-    assert lib_built.fmcw_abi_version() == 6
+    assert lib_built.fmcw_abi_version() == 7
     assert (cfg.compat_rtl, cfg.range_shift, cfg.spectrum_dtype) == (0, 0, L.SPEC_F32)
     assert b"gfx950" in lib_built.fmcw_version()
 
@@ -194,3 +194,23 @@ def test_null_arguments(lib_built):
     assert lib_built.fmcw_enqueue(None, None, 1, None, None, 0, None, None) == L.FMCW_EINVAL
     assert lib_built.fmcw_destroy(None) == L.FMCW_OK
     assert lib_built.fmcw_magnitude(None, None, 4, 0, None) == L.FMCW_EINVAL
+
+
+def test_comm_check_verdict(lib_built):
+    """fmcw_comm_create's collective check (round-4 verdict item 6): the verdict on the
+    all-reduced words {wire_cap, ~wire_cap, any rank failed} is the same on every rank -- a
+    failure on one rank fails every rank, and a wire_cap mismatch is EINVAL everywhere."""
+    W = (C.c_uint64 * 3)
+    m64 = (1 << 64) - 1
+    ok = W(16, m64 ^ 16, 0)
+    assert lib_built.fmcw_comm_check_decide_for_test(ok, 0, 16) == L.FMCW_OK
+    failed = W(16, m64 ^ 16, 1)
+    assert lib_built.fmcw_comm_check_decide_for_test(failed, 1, 16) == L.FMCW_ENOMEM
+    assert b"per rank" in lib_built.fmcw_last_error()
+    assert lib_built.fmcw_comm_check_decide_for_test(failed, 0, 16) == L.FMCW_ENOMEM
+    assert b"another rank" in lib_built.fmcw_last_error()
+    differ = W(32, m64 ^ 16, 0)
+    assert lib_built.fmcw_comm_check_decide_for_test(differ, 0, 16) == L.FMCW_EINVAL
+    assert lib_built.fmcw_comm_check_decide_for_test(differ, 0, 32) == L.FMCW_EINVAL
+    assert lib_built.fmcw_comm_check_decide_for_test(None, 0, 16) == L.FMCW_EINVAL
+    assert lib_built.fmcw_comm_fail_next_alloc_for_test(0) == L.FMCW_OK

@@ -172,3 +172,53 @@ def test_rccl_gather_host_side_world2():
         assert o["short_id"] == "ValueError"
         assert o["bad_rank"] == o["bad_world"] == o["zero_cap"] == o["huge_cap"] == "FMCW_EINVAL"
         assert o["valid"] == "FMCW_ENODEV"                  # all checks passed: stopped at the device
+
+
+def _worker_check_fail(rank, world, port, fail_rank, caps, q):
+    """fmcw_comm_create's collective check at world size 2 with one rank's buffer allocation
+    failing (round-4 verdict item 6): each rank builds its check words as the library does
+    ({wire_cap, ~wire_cap, failed}), the words are all-reduced with max -- over gloo here, RCCL in
+    the library -- and each rank takes the library's verdict on them.  No rank returns before the
+    collective, and every rank gets the same error."""
+    from fmcw import _lib as L
+    import ctypes as C
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lib = L.load()
+        failed = 1 if rank == fail_rank else 0
+        cap = caps[rank]
+        m64 = (1 << 64) - 1
+        # torch has no uint64 MAX all-reduce on gloo: max of (hi, lo) 32-bit halves is exact here
+        # (the halves of ~cap are all-ones in the high word for caps < 2^32)
+        words = [cap, m64 ^ cap, failed]
+        t = torch.tensor([[w >> 32, w & 0xffffffff] for w in words], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        red = (C.c_uint64 * 3)(*[int(t[i, 0]) << 32 | int(t[i, 1]) for i in range(3)])
+        rc = lib.fmcw_comm_check_decide_for_test(red, failed, cap)
+        q.put((rank, rc, lib.fmcw_last_error().decode()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_rank,caps,want", [(1, (64, 64), "ENOMEM"), (0, (64, 64), "ENOMEM"),
+                                                 (-1, (64, 64), "OK"), (-1, (64, 128), "EINVAL")])
+def test_comm_create_failure_fails_every_rank(fail_rank, caps, want):
+    from fmcw import _lib as L
+    code = {"OK": L.FMCW_OK, "ENOMEM": L.FMCW_ENOMEM, "EINVAL": L.FMCW_EINVAL}[want]
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_check_fail, args=(r, world, port, fail_rank, caps, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, rc, msg in res:
+        assert rc == code, (rank, rc, msg)
+        if want == "ENOMEM":
+            assert ("per rank" in msg) == (rank == fail_rank) and (("another rank" in msg) == (rank != fail_rank))
