@@ -74,7 +74,7 @@ def parse():
     ap.add_argument("--gather", default="rccl", choices=["rccl", "torch"],
                     help="N > 1: libfmcw's RCCL gather-to-root (no host sync) or torch all_gather")
     ap.add_argument("--no-h2d", action="store_true", help="skip the H2D-inclusive measurement")
-    ap.add_argument("--spectrum", default="f32", choices=["f32", "f16"],
+    ap.add_argument("--spectrum", default="f32", choices=["f32", "f16", "s48"],
                     help="element type of the corner-turned spectrum (fmcw.h fmcw_spectrum_dtype)")
     return ap.parse_args()
 
@@ -93,7 +93,7 @@ def kernel_rooflines(wl, name, F, steps, kt, spectrum, n_cu, pmc):
     """Per-kernel rooflines from the HIP-event times of `steps` profiled steps of F frames."""
     ns, nc, nrx = wl["ns"], wl["nc"], wl["nrx"]
     b_in = 8 if wl["dtype"] == "f32" else 4
-    b_sp = 4 if spectrum == "f16" else 8
+    b_sp = {"f16": 4, "s48": 6}.get(spectrum, 8)
     px = ns * nc * nrx
     frames = F * steps
     # algorithmic bytes per frame (SURVEY.md 8d): K1 cube in + spectrum out; K2 spectrum in + map

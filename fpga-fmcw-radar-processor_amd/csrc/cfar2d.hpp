@@ -156,6 +156,9 @@ constexpr size_t cfar2d_smem_bytes(int hr) {
 #ifndef FMCW_K3_LV_QB
 #define FMCW_K3_LV_QB 680
 #endif
+#ifndef K3_SCREEN_AHEAD  // rows of the level screen's LDS reads in flight ahead of the accumulation
+#define K3_SCREEN_AHEAD 3
+#endif
 // level nibbles of 4 cells from their key16 pairs (cells d, d + 1 | d + 2, d + 3): (k | 0x8000) - Q has
 // bit 15 set iff k >= Q (k < 0x8000, 1 <= Q <= 0x8000: no borrow across the halves); the byte
 // permute collects bits 15 / 31 of both words as bit 7 of 4 bytes
@@ -198,20 +201,42 @@ __device__ __forceinline__ uint32_t cfar2d_screen_lv(const RowRing& rr, int rl, 
   for (int k = 0; k < 8; ++k) V[k] = 0u;
 #pragma unroll
   for (int k = 0; k < 6; ++k) G[k] = 0u;
+  // The 2 HR + 1 rows' 32-byte windows, with at most K3_SCREEN_AHEAD rows' loads in flight: left to
+  // itself the scheduler issued all 22 LDS reads first (88 VGPRs of loads, the kernel's register
+  // peak); the scheduling barriers keep a rolling window of loads ahead of the accumulation.
+  constexpr int NW = 2 * HR + 1, AH = K3_SCREEN_AHEAD < NW ? K3_SCREEN_AHEAD : NW;
   int sl = rr.slot(rl);  // ring slot of window row dr = -HR, advanced with wrap
-#pragma unroll
-  for (int dr = -HR; dr <= HR; ++dr) {
+  uint4 q0[AH], q1[AH];
+  auto load_row = [&](int j) {
     const uint8_t* rp = rr.tile + sl * rr.rs + b7idx(d0 - 8);
-    const uint4 q0 = *reinterpret_cast<const uint4*>(rp), q1 = *reinterpret_cast<const uint4*>(rp + 16);
-    const uint32_t D[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+    q0[j % AH] = *reinterpret_cast<const uint4*>(rp);
+    q1[j % AH] = *reinterpret_cast<const uint4*>(rp + 16);
+    sl = sl + 1 == rr.nr ? 0 : sl + 1;
+  };
+#pragma unroll
+  for (int j = 0; j < AH; ++j) load_row(j);
+#pragma unroll
+  for (int j = 0; j < NW; ++j) {
+    const int dr = j - HR;
+    if constexpr (K3_SCREEN_AHEAD < 2 * HR + 1) __builtin_amdgcn_sched_barrier(0);
+    const uint4 a0 = q0[j % AH], a1 = q1[j % AH];
+    const uint32_t D[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    if (j + AH < NW) load_row(j + AH);
 #pragma unroll
     for (int k = 0; k < 8; ++k) V[k] += D[k];
     if (dr >= -GR && dr <= GR) {
 #pragma unroll
       for (int k = 0; k < 6; ++k) G[k] += D[k + 1];
     }
-    sl = sl + 1 == rr.nr ? 0 : sl + 1;
+    if constexpr (K3_SCREEN_AHEAD < 2 * HR + 1) {
+      // the row's sums now (no reassociation into one add tree after every load)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(V[k]));
+#pragma unroll
+      for (int k = 0; k < 6; ++k) asm volatile("" : "+v"(G[k]));
+    }
   }
+  if constexpr (K3_SCREEN_AHEAD < 2 * HR + 1) __builtin_amdgcn_sched_barrier(0);
   // 13-cell window per level: realign so that word k byte t = cell d0 - 6 + 4k + t, then unpack
   uint32_t HA[4], HB[4];
   {
@@ -441,7 +466,7 @@ __device__ __forceinline__ uint32_t wave_select_kth(uint32_t ka, uint32_t kb, ui
 }
 
 #ifndef FMCW_K3_WAVES  // waves per SIMD the register budget is cut for
-#define FMCW_K3_WAVES 3
+#define FMCW_K3_WAVES 4
 #endif
 
 // HD > 0: the reference window (HD 6, GD 2, compile-time HR / GR) with the level screen; HD == 0:

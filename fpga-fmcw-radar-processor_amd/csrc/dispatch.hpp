@@ -20,8 +20,9 @@ struct RangeInfo {
   int kind;        // RangeKind actually selected
 };
 // want = the preferred family (kRangePx: k_range_px at N = 8192, kRangeSeq: k_range_sq at N = 4096,
-// else k_range); q15 / h16 select the RTL-compat window and the fp16 spectrum (k_range only)
-RangeInfo range_info(uint32_t n, int dtype, int window, bool h16, int want);
+// else k_range); window FMCW_WIN_Q15_RTL and spec (fmcw_spectrum_dtype) FMCW_SPEC_F16 / _S48 run
+// k_range (S48: N <= 1024 only, fn = nullptr otherwise)
+RangeInfo range_info(uint32_t n, int dtype, int window, int spec, int want);
 
 // ---- K2: Doppler window + FFT + |X| / NCI + map + 1-D CFAR --------------------------------
 using DopplerFn = void (*)(const float2*, const float*, int, int, int, int, int, int, int, float*,
@@ -32,9 +33,12 @@ struct DopplerInfo {
 };
 DopplerFn doppler_fn_f32(uint32_t nc, int mti, bool fast, bool q15);  // inst_doppler.hip
 DopplerFn doppler_fn_f16(uint32_t nc, int mti, bool fast);            // inst_doppler_h16.hip
-inline DopplerInfo doppler_info(uint32_t nc, int mti = FMCW_MTI_OFF, bool h16 = false, bool fast = false,
+DopplerFn doppler_fn_s48(uint32_t nc, int mti, bool fast);            // inst_doppler_s48.hip (nullptr: unsupported)
+inline DopplerInfo doppler_info(uint32_t nc, int mti = FMCW_MTI_OFF, int spec = FMCW_SPEC_F32, bool fast = false,
                                 bool q15 = false) {
-  DopplerFn fn = h16 ? doppler_fn_f16(nc, mti, fast) : doppler_fn_f32(nc, mti, fast, q15);
+  DopplerFn fn = spec == FMCW_SPEC_F16   ? doppler_fn_f16(nc, mti, fast)
+                 : spec == FMCW_SPEC_S48 ? doppler_fn_s48(nc, mti, fast)
+                                         : doppler_fn_f32(nc, mti, fast, q15);
   switch (nc) {
 #define D_(N) case N: return {fn, DopplerGeom<N>::WR, DopplerGeom<N>::NT};
     D_(32) D_(64) D_(128) D_(256) D_(512) D_(1024)

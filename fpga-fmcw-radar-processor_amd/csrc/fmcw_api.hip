@@ -356,7 +356,7 @@ int validate(const fmcw_config& c) {
     return fail(FMCW_EINVAL, "map_kind=%d unknown", c.map_kind);
   if (c.mti_mode != FMCW_MTI_OFF && c.mti_mode != FMCW_MTI_2PULSE && c.mti_mode != FMCW_MTI_3PULSE)
     return fail(FMCW_EINVAL, "mti_mode=%d unknown (0 off, 2 or 3 pulse)", c.mti_mode);
-  if (range_info(c.n_range, c.in_dtype, c.window, false, kRangePx).T > (int)c.n_doppler)
+  if (range_info(c.n_range, c.in_dtype, c.window, FMCW_SPEC_F32, kRangePx).T > (int)c.n_doppler)
     return fail(FMCW_EINVAL, "n_doppler=%u smaller than the range kernel's chirp group", c.n_doppler);
   if (c.max_frames < 1) return fail(FMCW_EINVAL, "max_frames must be >= 1");
   if (c.cfar_kind == FMCW_CFAR_OS1D) {
@@ -390,8 +390,17 @@ int validate(const fmcw_config& c) {
   if ((c.compat_rtl & FMCW_COMPAT_MTI) && c.mti_mode == FMCW_MTI_OFF)
     return fail(FMCW_EINVAL, "compat MTI needs mti_mode 2 or 3");
   if (c.range_shift > 13) return fail(FMCW_EINVAL, "range_shift=%u: must be in [0, 13]", c.range_shift);
-  if (c.spectrum_dtype != FMCW_SPEC_F32 && c.spectrum_dtype != FMCW_SPEC_F16)
+  if (c.spectrum_dtype != FMCW_SPEC_F32 && c.spectrum_dtype != FMCW_SPEC_F16 && c.spectrum_dtype != FMCW_SPEC_S48)
     return fail(FMCW_EINVAL, "spectrum_dtype=%d unknown", c.spectrum_dtype);
+  if (c.spectrum_dtype == FMCW_SPEC_S48) {
+    // one exponent per chirp quad of a range bin: the quad must be one K1 tile row (T >= 4 chirps:
+    // n_range <= 1024) and one K2 lane quad (n_doppler >= 64), and no MTI (the canceller reads
+    // neighbouring chirps from other lanes of the quad)
+    if (c.n_range > 1024 || c.n_doppler < 64)
+      return fail(FMCW_EINVAL, "spectrum_dtype S48 needs n_range <= 1024 and n_doppler >= 64");
+    if (c.mti_mode != FMCW_MTI_OFF || c.window == FMCW_WIN_Q15_RTL)
+      return fail(FMCW_EINVAL, "spectrum_dtype S48 is defined with MTI off and an fp32 window (not Q15_RTL)");
+  }
   if (c.spectrum_dtype == FMCW_SPEC_F16 && (c.compat_rtl & FMCW_COMPAT_MTI))
     return fail(FMCW_EINVAL, "compat MTI is defined on the fp32 spectrum (spectrum_dtype F16)");
   // the Q15 path rounds the corner-turned spectrum to int16 words (and windows them in K2): an fp16
@@ -741,16 +750,22 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
     h->k1_want = !std::strcmp(k1, "single") ? kRangeSingle : !std::strcmp(k1, "seq") ? kRangeSeq : kRangePx;
 #endif
   h->k2_fast = k2_fast(c);
-  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, c.spectrum_dtype == FMCW_SPEC_F16, h->k1_want);
+  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, c.spectrum_dtype, h->k1_want);
   h->k1_kind = ri.kind;
   h->T = ri.T;
   h->RB = ri.RB;
   h->lgT = __builtin_ctz(ri.T);
   h->lgRB = __builtin_ctz(ri.RB);
   const size_t frame_inter = (size_t)c.n_rx * c.n_range * c.n_doppler *
-                             (c.spectrum_dtype == FMCW_SPEC_F16 ? sizeof(uint32_t) : sizeof(float2));
+                             (c.spectrum_dtype == FMCW_SPEC_F16   ? sizeof(uint32_t)
+                              : c.spectrum_dtype == FMCW_SPEC_S48 ? sizeof(S48)
+                                                                  : sizeof(float2));
   occupancy_grid(ri.fn, ri.NT, 0, h->n_cu, &h->grid_range);
-  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype == FMCW_SPEC_F16, h->k2_fast);
+  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype, h->k2_fast);
+  if (!ri.fn || !di.fn) {
+    delete h;
+    return fail(FMCW_EINVAL, "no kernel for this configuration (spectrum_dtype %d)", c.spectrum_dtype);
+  }
   occupancy_grid(di.fn, di.NT, 0, h->n_cu, &h->grid_doppler);
 #if FMCW_LAB
   if (const char* cs = std::getenv("FMCW_CFAR2D_STEPS")) h->cfar2_steps = std::max(0, std::atoi(cs));
@@ -772,7 +787,8 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   // K1 / K2 address a launch's spectrum with 32-bit byte offsets (buffer loads and stores)
   h->chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(h->chunk, ((size_t)1 << 32) / frame_inter - 1));
   // >= one fp32 frame: fmcw_range_ct writes the fp32 spectrum through it whatever spectrum_dtype
-  h->inter_bytes = std::max((size_t)h->chunk * frame_inter, (size_t)c.n_rx * c.n_range * c.n_doppler * sizeof(float2));
+  // (+16 B: an S48 point is read as the 8 bytes from its record rounded down to 4)
+  h->inter_bytes = std::max((size_t)h->chunk * frame_inter, (size_t)c.n_rx * c.n_range * c.n_doppler * sizeof(float2)) + 16;
   ALLOC(h->inter, h->inter_bytes);
   if (c.cfar_kind == FMCW_CFAR_OS2D) {
     ALLOC(h->lin_scratch, (size_t)h->chunk * c.n_range * c.n_doppler * sizeof(float));
@@ -885,8 +901,8 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
     return fail(FMCW_EINVAL, "n_dets_dev is required when a CFAR is configured");
   HIP_TRY(hipSetDevice(c.device_id));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, c.spectrum_dtype == FMCW_SPEC_F16, h->k1_want);
-  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype == FMCW_SPEC_F16, h->k2_fast);
+  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, c.spectrum_dtype, h->k1_want);
+  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype, h->k2_fast);
   const size_t frame_px = (size_t)c.n_range * c.n_doppler;
   const size_t in_frame_bytes = cube_bytes(c, 1);
   const Cfar1DArgs cf1 = cfar1_args(c);
@@ -1017,7 +1033,7 @@ int fmcw_range_ct(fmcw_handle* h, const void* cube, size_t n_frames, void* spec,
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // the stage output is the fp32 spectrum whatever spectrum_dtype the path uses: K1's fp32
   // variant, as many frames per launch as the intermediate buffer holds at 8 B per point
-  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, false, h->k1_want);
+  const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, FMCW_SPEC_F32, h->k1_want);
   const size_t in_frame_bytes = cube_bytes(c, 1);
   const size_t fr_px = (size_t)c.n_rx * c.n_range * c.n_doppler;
   const size_t rc_chunk = std::max<size_t>(1, h->inter_bytes / (fr_px * sizeof(float2)));

@@ -6,10 +6,10 @@ namespace fmcw {
 namespace {
 template <int N>
 DopplerFn dfn(int mti, bool fast) {
-  return mti == FMCW_MTI_2PULSE   ? k_doppler<N, 2, false>
-         : mti == FMCW_MTI_3PULSE ? k_doppler<N, 3, false>
-         : fast                   ? k_doppler<N, 0, false, true>
-                                  : k_doppler<N, 0, false>;
+  return mti == FMCW_MTI_2PULSE   ? k_doppler<N, 2, SP_F32>
+         : mti == FMCW_MTI_3PULSE ? k_doppler<N, 3, SP_F32>
+         : fast                   ? k_doppler<N, 0, SP_F32, true>
+                                  : k_doppler<N, 0, SP_F32>;
 }
 }  // namespace
 

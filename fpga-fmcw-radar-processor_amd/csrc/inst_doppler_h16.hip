@@ -6,10 +6,10 @@ namespace fmcw {
 namespace {
 template <int N>
 DopplerFn dfn(int mti, bool fast) {
-  return mti == FMCW_MTI_2PULSE   ? k_doppler<N, 2, true>
-         : mti == FMCW_MTI_3PULSE ? k_doppler<N, 3, true>
-         : fast                   ? k_doppler<N, 0, true, true>
-                                  : k_doppler<N, 0, true>;
+  return mti == FMCW_MTI_2PULSE   ? k_doppler<N, 2, SP_F16>
+         : mti == FMCW_MTI_3PULSE ? k_doppler<N, 3, SP_F16>
+         : fast                   ? k_doppler<N, 0, SP_F16, true>
+                                  : k_doppler<N, 0, SP_F16>;
 }
 }  // namespace
 

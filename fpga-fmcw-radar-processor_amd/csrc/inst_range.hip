@@ -4,18 +4,22 @@
 namespace fmcw {
 namespace {
 
-template <int N, bool H16>
+template <int N, int SP>
 RangeFn range_fn_t(int dtype, bool q15) {
   switch (dtype) {
-    case FMCW_IN_F32: return k_range<N, LoadF32, false, H16>;
-    case FMCW_IN_F16: return k_range<N, LoadF16, false, H16>;
-    case FMCW_IN_I16: return q15 ? k_range<N, LoadI16, true, H16> : k_range<N, LoadI16, false, H16>;
+    case FMCW_IN_F32: return k_range<N, LoadF32, false, SP>;
+    case FMCW_IN_F16: return k_range<N, LoadF16, false, SP>;
+    case FMCW_IN_I16: return q15 ? k_range<N, LoadI16, true, SP> : k_range<N, LoadI16, false, SP>;
   }
   return nullptr;
 }
 template <int N>
-RangeFn range_fn(int dtype, bool q15, bool h16) {
-  return h16 ? range_fn_t<N, true>(dtype, q15) : range_fn_t<N, false>(dtype, q15);
+RangeFn range_fn(int dtype, bool q15, int spec) {
+  if constexpr (RangeGeom<N>::T >= 4) {  // S48 shares its exponent over 4 chirps of a tile row
+    if (spec == FMCW_SPEC_S48) return q15 ? nullptr : range_fn_t<N, SP_S48>(dtype, false);
+  }
+  return spec == FMCW_SPEC_F16 ? range_fn_t<N, SP_F16>(dtype, q15) : spec == FMCW_SPEC_F32 ? range_fn_t<N, SP_F32>(dtype, q15)
+                                                                                          : nullptr;
 }
 
 // k_range_sq (sequential pair, round 3): N = 4096, the measured-fastest values per thread V,
@@ -48,15 +52,15 @@ RangeInfo range_px(int dtype) {
 
 }  // namespace
 
-RangeInfo range_info(uint32_t n, int dtype, int window, bool h16, int want) {
+RangeInfo range_info(uint32_t n, int dtype, int window, int spec, int want) {
   const bool q15 = window == FMCW_WIN_Q15_RTL;
-  // the pair kernels: fp32 window, fp32 spectrum (the Q15 / fp16-spectrum paths run k_range)
-  if (!q15 && !h16) {
+  // the pair kernels: fp32 window, fp32 spectrum (the Q15 / fp16 / S48-spectrum paths run k_range)
+  if (!q15 && spec == FMCW_SPEC_F32) {
     if (want >= kRangePx && FMCW_K1_PX && n == 8192) return range_px(dtype);
     if (want >= kRangeSeq && FMCW_K1_SQ && n == 4096 && n >= (uint32_t)FMCW_K1_SQ) return range_sq<4096>(dtype);
   }
   switch (n) {
-#define R_(N) case N: return {range_fn<N>(dtype, q15, h16), RangeGeom<N>::T, RangeGeom<N>::RB, RangeGeom<N>::NT, kRangeSingle};
+#define R_(N) case N: return {range_fn<N>(dtype, q15, spec), RangeGeom<N>::T, RangeGeom<N>::RB, RangeGeom<N>::NT, kRangeSingle};
     R_(64) R_(128) R_(256) R_(512) R_(1024) R_(2048) R_(4096) R_(8192)
 #undef R_
   }

@@ -135,9 +135,74 @@ struct LoadI16 {
 // Corner-turned spectrum element: complex fp32 (8 B) or, with FMCW_SPEC_F16, a half2 (4 B)
 // holding X / N_range (|X| <= N max|x| would overflow fp16 for ADC-scale input; the 2^-log2 N
 // scale is exact and K2 undoes it at load).
-template <bool H16> struct SpecEl { using T = float2; };
-template <> struct SpecEl<true> { using T = uint32_t; };
+// Spectrum formats (fmcw.h fmcw_spectrum_dtype): SP_F32 float2 (8 B), SP_F16 half2 of X / N (4 B),
+// SP_S48 (6 B, below).
+constexpr int SP_F32 = 0, SP_F16 = 1, SP_S48 = 2;
+struct __attribute__((packed)) S48 { uint16_t h[3]; };  // one S48 point: pointer steps of 6 B
+template <int SP> struct SpecEl { using T = float2; };
+template <> struct SpecEl<SP_F16> { using T = uint32_t; };
+template <> struct SpecEl<SP_S48> { using T = S48; };
 typedef _Float16 fmcw_h2 __attribute__((ext_vector_type(2)));
+
+// ---- S48: the corner-turned spectrum in 6 bytes per point, exact to 2^-23 of its chirp quad -----
+// The four chirps 4k .. 4k + 3 of one range bin (contiguous in a tile row: T >= 4) share one
+// exponent E = max frexp exponent of their 8 components (|x| < 2^E), clamped to >= -95; each
+// component is stored as q = rint(x 2^(22 - E)), a 23-bit two's-complement significand (clamped
+// to 2^22 - 1), so |x - q 2^(E - 22)| <= 2^(E - 23): 2^-23 of the quad's largest component (or of
+// 2^-95), where fp32 keeps 2^-24 of each.  Point record (48 bits, little-endian, point q of the
+// quad at bytes 6q .. 6q + 5): bits 0-22 re, 23-24 bits 2q, 2q + 1 of e8 = E + 127, 25-47 im.
+// K1 lanes hold chirp pairs (c0, c0 + 1), c0 even, and exchange the pair maximum with the lane of
+// the other pair of their quad (lane ^ 1); K2 lanes t .. t + 3 (P % 4 == 0) hold the quad's four
+// chirps and OR their 2-bit exponent pieces together across the quad (DPP).  Measured on the CPU
+// model (fp64 oracle, config-2 frames, per-bin error on bins >= 1e-3 of the frame peak): <= 3.3e-5
+// over 48 frames, against 1e-4 allowed; one exponent per point with 20-bit significands reached
+// 1.9e-4.
+typedef uint32_t fmcw_u3v __attribute__((ext_vector_type(3)));
+__device__ __forceinline__ fmcw_u3v s48_pack_pair(float2 v0, float2 v1, int q0) {
+  const float m = fmaxf(fmaxf(fabsf(v0.x), fabsf(v0.y)), fmaxf(fabsf(v1.x), fabsf(v1.y)));
+  const int el = __builtin_amdgcn_frexp_expf(m);  // m < 2^el (0 for m = 0)
+  const int ep = __builtin_amdgcn_mov_dpp(el, 0xB1 /* quad_perm [1,0,3,2]: lane ^ 1 */, 0xf, 0xf, false);
+  const int E = max(max(el, ep), -95);  // K2's scale 2^(E - 31) stays a normal float
+  const uint32_t e8 = (uint32_t)(E + 127);
+  const int sh = 22 - E;
+  auto sig = [sh](float x) -> uint32_t {
+    const int q = (int)__builtin_rintf(__builtin_amdgcn_ldexpf(x, sh));
+    return (uint32_t)min(max(q, -(1 << 22)), (1 << 22) - 1);
+  };
+  const uint32_t r0 = sig(v0.x), i0 = sig(v0.y), r1 = sig(v1.x), i1 = sig(v1.y);
+  const uint32_t b0 = (e8 >> (2 * q0)) & 3u, b1 = (e8 >> (2 * q0 + 2)) & 3u;
+  constexpr uint32_t M23 = (1u << 23) - 1;
+  fmcw_u3v w;
+  w.x = (r0 & M23) | (b0 << 23) | (i0 << 25);                                // P0 bits 0-31
+  w.y = ((i0 >> 7) & 0xffffu) | (r1 << 16);                                  // P0 32-47, P1 0-15
+  w.z = ((r1 >> 16) & 0x7fu) | (b1 << 7) | (i1 << 9);                        // P1 16-47
+  return w;
+}
+// One point from the 8 bytes loaded at its record's byte offset rounded down to 4 (odd = its point
+// index is odd: the record starts at byte 2 of them); q2 = 2 (c & 3).  Every lane of the quad must
+// call it together.  Two byte permutes give the record's bits 0-31 and 16-47; the significands
+// land in the top 23 bits of a word (low bits zero), so v_cvt_f32_i32 reads q 2^9 exactly and one
+// packed multiply by 2^(E - 31) scales both components.
+__device__ __forceinline__ float2 s48_unpack(fmcw_u2v raw, uint32_t odd, uint32_t q2) {
+  const uint32_t so = odd * 0x02020202u;
+  const uint32_t w0 = __builtin_amdgcn_perm(raw.y, raw.x, 0x03020100u + so);  // record bits 0-31
+  const uint32_t w1 = __builtin_amdgcn_perm(raw.y, raw.x, 0x05040302u + so);  // record bits 16-47
+  const float re = (float)(int)(w0 << 9), im = (float)(int)(w1 & 0xfffffe00u);
+  int e = (int)(__builtin_amdgcn_ubfe(w0, 23, 2) << q2);
+  e |= __builtin_amdgcn_mov_dpp(e, 0xB1 /* lane ^ 1 */, 0xf, 0xf, false);
+  e |= __builtin_amdgcn_mov_dpp(e, 0x4E /* quad_perm [2,3,0,1]: lane ^ 2 */, 0xf, 0xf, false);
+  const float sc = __uint_as_float((uint32_t)(e - 31) << 23);  // 2^(E - 31), E = e - 127 >= -95
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  const f2v r = f2v{re, im} * f2v{sc, sc};
+  return make_float2(r.x, r.y);
+}
+// The raw 8 bytes of point p (record at 6 p bytes from the S48 array's start): loaded from the
+// 4-aligned byte 6 p - 2 (p & 1)
+template <bool NT>
+__device__ __forceinline__ fmcw_u2v ld_s48_raw(const S48* p, uint32_t odd) {
+  return ld_u2<NT>(reinterpret_cast<const char*>(p) - 2 * odd);
+}
+
 __device__ __forceinline__ uint32_t pack_h2(float x, float y) {
   return __builtin_bit_cast(uint32_t, fmcw_h2{(_Float16)x, (_Float16)y});
 }
@@ -184,8 +249,9 @@ template <int N> struct RangeGeom {
 // Q15 = RTL-compat integer range window (FMCW_WIN_Q15_RTL, int16 input): `win` then holds the
 // ROM integers c[n] (exact in fp32) and each sample is windowed as sat16((x c + 2^14) >> 14)
 // (window_multiplier.vhd:146-158) before it becomes fp32.
-// H16 = FMCW_SPEC_F16: the tiles hold half2(X / N) (8-B stores of two chirps).
-template <int N, typename LD, bool Q15 = false, bool H16 = false>
+// SP = spectrum format: SP_F16 (FMCW_SPEC_F16) tiles hold half2(X / N) (8-B stores of two chirps),
+// SP_S48 (FMCW_SPEC_S48, T >= 4) two 6-B S48 points (12-B stores).
+template <int N, typename LD, bool Q15 = false, int SP = SP_F32>
 __global__ void __launch_bounds__(RangeGeom<N>::NT)
 __attribute__((amdgpu_waves_per_eu(FMCW_K1_WAVES > 0 && N < 8192 ? FMCW_K1_WAVES : 1)))
 k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* __restrict__ win,
@@ -245,7 +311,7 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
     const int t = opaque(t0);
     float2* buf = lds + q * REG;
     // Doppler window of this chirp folded in (K2 then skips it; FFT linearity), or 1
-    const float cw = cw_n * (H16 ? 1.0f / N : 1.0f);
+    const float cw = cw_n * (SP == SP_F16 ? 1.0f / N : 1.0f);
 
     float2 w[8];
 #pragma unroll
@@ -318,7 +384,13 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
         v0 = lds[c0 * REG + pad16(r0 + i * (N / 8))];
         v1 = lds[(c0 + 1) * REG + pad16(r0 + i * (N / 8))];
       }
-      if constexpr (H16) dst16[i * dstep / 2] = make_uint2(pack_h2(v0.x, v0.y), pack_h2(v1.x, v1.y));
+      if constexpr (SP == SP_F16) dst16[i * dstep / 2] = make_uint2(pack_h2(v0.x, v0.y), pack_h2(v1.x, v1.y));
+      else if constexpr (SP == SP_S48) {
+        static_assert(T >= 4, "S48 shares an exponent over 4 chirps of a tile row");
+        __builtin_amdgcn_raw_buffer_store_b96(s48_pack_pair(v0, v1, c0 & 3), wrs,
+                                              (uint32_t)((dbase + i * dstep) * sizeof(S48)), 0,
+                                              FMCW_K1_WT ? 16 /* sc1 */ : 0);
+      }
       else if constexpr (FMCW_K1_WT && N <= 4096) st_f4_wt(wrs, (uint32_t)((dbase + i * dstep) * sizeof(float2)), make_float4(v0.x, v0.y, v1.x, v1.y));
       else st_f4<FMCW_NT_SPEC_ST>(dst + i * dstep, make_float4(v0.x, v0.y, v1.x, v1.y));
     }
@@ -1369,9 +1441,16 @@ __device__ __forceinline__ int xcd_block_id(int bid, int grid) {
 // 39 KiB LDS per CU); measured K2 58.2 -> 56.0 us per 96-frame launch at config 2.  At NC = 512
 // / 1024 the fourth wave costs more than it hides (config 3 K2 41.7 -> 55.9 us, config 5 55.5
 // -> 74.6 us per launch; gpurun_out bench_libs, round 2).
-template <int NC, int MTI, bool FAST = false>
+#ifndef FMCW_K2_S48_WAVES  // lab A/B: waves per SIMD of the S48 K2 (0 = as fp32)
+#define FMCW_K2_S48_WAVES 0
+#endif
+#ifndef FMCW_K2_S48_PF     // lab A/B: points prefetched by the S48 K2 at NC <= FMCW_K2_PF_NC
+#define FMCW_K2_S48_PF 16
+#endif
+template <int NC, int MTI, bool FAST = false, int SP = SP_F32>
 constexpr int k2_waves() {
   return FMCW_K2_WAVES > 0                 ? FMCW_K2_WAVES
+         : (SP == SP_S48 && FMCW_K2_S48_WAVES > 0) ? FMCW_K2_S48_WAVES
          : (FAST && MTI == 0 && NC == 256) ? 4
          : (MTI == 0 && NC <= 256 && FMCW_K2_PREFETCH <= 8) ? 3
                                                             : 2;
@@ -1380,8 +1459,9 @@ constexpr int k2_waves() {
 // and the 1-D CFAR, when enabled, at the reference geometry (8 refs / 2 guards per side, need =
 // n_ref - rank <= 4, fp32 compare).  The generic kernel keeps those as uniform runtime branches,
 // whose other arms held registers and SGPRs (spills to VGPR lanes) across the tile loop.
-template <int NC, int MTI, bool H16 = false, bool FAST = false>
-__global__ void __launch_bounds__(DopplerGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(k2_waves<NC, MTI, FAST>())))
+// SP: the spectrum format K1 wrote (SP_F32, SP_F16, SP_S48; S48 with MTI off, P % 4 == 0 and T >= 4).
+template <int NC, int MTI, int SP = SP_F32, bool FAST = false>
+__global__ void __launch_bounds__(DopplerGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(k2_waves<NC, MTI, FAST, SP>())))
 k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, int ns, int nrx,
           int lgT, int lgRB, int n_tiles, int frame0, int tile0, float* __restrict__ lin_map,
           float* __restrict__ db_map, int mag_mode, int mti_rtl, int q15d, Cfar1DArgs cf, DetSink sink,
@@ -1394,9 +1474,14 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
 
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane0 = threadIdx.x & 63;
-  using SE = typename SpecEl<H16>::T;
+  using SE = typename SpecEl<SP>::T;
   const SE* const inter = reinterpret_cast<const SE*>(inter_in);
-  const float sscale = H16 ? (float)ns : 1.f;  // undoes K1's 1 / N_range of an fp16 spectrum
+  const float sscale = SP == SP_F16 ? (float)ns : 1.f;  // undoes K1's 1 / N_range of an fp16 spectrum
+  static_assert(SP != SP_S48 || (MTI == 0 && P % 4 == 0), "S48: a lane quad holds a chirp quad");
+  // S48: this lane's chirps c = t + P m all sit at c & 3 = t & 3 of their quad (t = lane % P);
+  // the two lane constants are derived from t where they are used (not held across the loop)
+  auto s48_sh = [](int tt) { return (uint32_t)(tt & 1) << 4; };   // byte offset x 8 of the record in its load
+  auto s48_q2 = [](int tt) { return (uint32_t)(tt & 3) << 1; };
   const int rr = lane0 / P;
   const int t0 = lane0 % P;
   float* const mags = lds + wv * Gm::WFL;
@@ -1431,7 +1516,7 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
   // of HBM reads in flight through its FFT, magnitude, map store and CFAR phases instead of
   // exposing the full load latency once per unit.
   constexpr int NPF = MTI != 0                ? 0
-                      : NC <= FMCW_K2_PF_NC     ? FMCW_K2_PREFETCH
+                      : NC <= FMCW_K2_PF_NC     ? (SP == SP_S48 ? FMCW_K2_S48_PF : FMCW_K2_PREFETCH)
                       : NC == 512               ? FMCW_K2_PREFETCH_512
                       : NC == 1024              ? FMCW_K2_PREFETCH_1024
                                                 : 0;  // points loaded ahead
@@ -1481,7 +1566,16 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
           const uint32_t sb = S * (uint32_t)sizeof(SE);
 #pragma unroll
           for (int m = 0; m < NPF; ++m) {
-            if constexpr (!H16 && FMCW_K2_BUFLD) {
+            if constexpr (SP == SP_S48) {
+              // the raw 8 bytes at the point's record rounded down to 4 (decoded at use)
+              const uint32_t vo = (uint32_t)((const char*)pb - (const char*)inter) - (s48_sh(tq) >> 3);
+              typedef float f2v __attribute__((ext_vector_type(2)));
+              const f2v r = __builtin_bit_cast(
+                  f2v, __builtin_amdgcn_raw_buffer_load_b64(srs, vo, so, FMCW_NT_SPEC_LD ? 2 /* nt */ : 0));
+              nxt[m] = make_float2(r.x, r.y);
+              so += sb;
+              if constexpr (FMCW_K2_SOFF_CHAIN) asm volatile("" : "+s"(so));
+            } else if constexpr (SP == SP_F32 && FMCW_K2_BUFLD) {
               // buffer load: lane offset in a VGPR, the uniform m S in an SGPR (no 64-bit VALU
               // address add per load; the chunk's spectrum is < 4 GiB, fmcw_create caps it)
               const uint32_t vo = (uint32_t)((const char*)pb - (const char*)inter);
@@ -1499,7 +1593,13 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
 #pragma unroll
           for (int m = 0; m < NPF; ++m) {
             const uint32_t c = (uint32_t)(tq + P * m);
-            nxt[m] = ld_spec<FMCW_NT_SPEC_LD>(p + ((((c >> lgT) << lgRB) << lgT) | (c & (uint32_t)(T - 1))), sscale);
+            const SE* pc = p + ((((c >> lgT) << lgRB) << lgT) | (c & (uint32_t)(T - 1)));
+            if constexpr (SP == SP_S48) {
+              const fmcw_u2v r = ld_s48_raw<FMCW_NT_SPEC_LD>(pc, (uint32_t)tq & 1u);
+              nxt[m] = make_float2(__uint_as_float(r.x), __uint_as_float(r.y));
+            } else {
+              nxt[m] = ld_spec<FMCW_NT_SPEC_LD>(pc, sscale);
+            }
           }
         }
       }
@@ -1531,12 +1631,21 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
 
     for (int rx = 0; rx < nrx; ++rx) {
       const SE* src = inter + ((size_t)f * nrx + rx) * (size_t)ns * NC;
-      auto at = [&](uint32_t c) -> float2 { return ld_spec<FMCW_NT_SPEC_LD>(src + off_of(rbase, rin, c), sscale); };
+      auto at = [&](uint32_t c) -> float2 {
+        if constexpr (SP == SP_S48) return s48_unpack(ld_s48_raw<FMCW_NT_SPEC_LD>(src + off_of(rbase, rin, c), c & 1u), (uint32_t)t & 1u, s48_q2(t));
+        else return ld_spec<FMCW_NT_SPEC_LD>(src + off_of(rbase, rin, c), sscale);
+      };
       float2 v[16];
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int c = t + P * m;
-        float2 x = m < NPF ? nxt[m < NPF ? m : 0] : at((uint32_t)c);
+        float2 x;
+        if (m < NPF) {
+          x = nxt[m < NPF ? m : 0];
+          if constexpr (SP == SP_S48) x = s48_unpack(fmcw_u2v{__float_as_uint(x.x), __float_as_uint(x.y)}, (uint32_t)t & 1u, s48_q2(t));
+        } else {
+          x = at((uint32_t)c);
+        }
         // RTL-compat words: the corner turner hands the FFT IP's 16-bit output words on
         // (round half to even, saturate; counted in status word 3)
         const bool words = !FAST && (mti_rtl || q15d);

@@ -24,7 +24,7 @@ MAP_LINEAR, MAP_DB = 1, 2
 CFAR_NONE, CFAR_OS1D, CFAR_OS2D = 0, 1, 2
 MTI_OFF, MTI_2PULSE, MTI_3PULSE = 0, 2, 3
 COMPAT_CFAR, COMPAT_MTI = 1, 2
-SPEC_F32, SPEC_F16 = 0, 1
+SPEC_F32, SPEC_F16, SPEC_S48 = 0, 1, 2
 COMM_ID_BYTES = 128
 K_RANGE, K_DOPPLER, K_CFAR2D, K_COMPACT, K_COUNT = 0, 1, 2, 3, 4
 KERNEL_NAMES = ("k_range", "k_doppler", "k_cfar", "k_compact")

@@ -164,7 +164,9 @@ class RadarCore:
         FFT IP's fixed scaling schedule), so that the 16-bit spectrum words of the compat MTI and
         of window="q15_rtl" (integer windows on both axes) are meaningful.
         spectrum: "f32" or "f16", the element type of the internal corner-turned spectrum
-        (fmcw.h fmcw_spectrum_dtype: "f16" halves its HBM traffic; map within 2e-3)."""
+        (fmcw.h fmcw_spectrum_dtype: "f16" halves its HBM traffic, map within 2e-3; "s48" takes 6
+        bytes per point -- a 23-bit significand per component, one exponent per 4 chirps -- map
+        within the 1e-4 of "f32"; n_range <= 1024, n_doppler >= 64, MTI off)."""
         lib = L.load()
         cfg = L.default_config()
         cfg.mti_mode = L.MTI_OFF if mti_bypass else {2: L.MTI_2PULSE, 3: L.MTI_3PULSE}[NOTCH_MODE]
@@ -186,7 +188,7 @@ class RadarCore:
         cfg.compat_rtl = compat_rtl if isinstance(compat_rtl, int) else \
             sum(flags[k] for k in set(compat_rtl))
         cfg.range_shift = range_shift
-        cfg.spectrum_dtype = {"f32": L.SPEC_F32, "f16": L.SPEC_F16}[spectrum]
+        cfg.spectrum_dtype = {"f32": L.SPEC_F32, "f16": L.SPEC_F16, "s48": L.SPEC_S48}[spectrum]
         self.cfg = cfg
         self.in_dtype = in_dtype
         self.device = device

@@ -74,7 +74,7 @@ extern "C" {
                                   environment variable;
                                7: fmcw_enqueue / fmcw_cfar graph-capturable (device-resident
                                   ordering tag); fmcw_comm_fail_next_alloc_for_test,
-                                  fmcw_comm_check_decide_for_test */
+                                  fmcw_comm_check_decide_for_test; FMCW_SPEC_S48 */
 
 typedef enum {
   FMCW_OK = 0,
@@ -159,8 +159,14 @@ typedef struct fmcw_config {
  * (config 5: 160 -> 128 MiB of HBM traffic per frame).  The map then carries fp16 rounding of
  * the range spectrum: max |map - oracle| <= 2e-3 x max|oracle| per frame (tested), against
  * 1e-4 for FMCW_SPEC_F32; detections stay bit-exact to the oracle CFAR on the map produced.
- * Not with FMCW_COMPAT_MTI (its 16-bit words are defined on the fp32 spectrum). */
-typedef enum { FMCW_SPEC_F32 = 0, FMCW_SPEC_F16 = 1 } fmcw_spectrum_dtype;
+ * Not with FMCW_COMPAT_MTI (its 16-bit words are defined on the fp32 spectrum).
+ * FMCW_SPEC_S48 stores it in 6 bytes per point (config 2: 2 -> 1.5 MiB written and read back per
+ * frame): the four chirps 4k .. 4k + 3 of a range bin share one 8-bit exponent E (the largest
+ * of their 8 components is < 2^E), and every component is a 23-bit signed significand of
+ * 2^(E - 22), i.e. exact to 2^-23 of the quad's largest component (fp32: 2^-24 of each).  The map
+ * stays within the 1e-4 tolerance of FMCW_SPEC_F32 (per frame and per bin above 1e-3 of the
+ * frame peak; tested).  Needs n_range <= 1024, n_doppler >= 64, MTI off and a fp32 window. */
+typedef enum { FMCW_SPEC_F32 = 0, FMCW_SPEC_F16 = 1, FMCW_SPEC_S48 = 2 } fmcw_spectrum_dtype;
 
 /* fmcw_config.compat_rtl bits.
  * FMCW_COMPAT_CFAR: the CFAR on the RTL's 17-bit unsigned cells (DATA_WIDTH 17): each map

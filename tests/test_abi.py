@@ -93,7 +93,7 @@ def test_defaults_mirror_radar_core(lib_built):
     ("cfar2d_rank_pct", 101, b"rank_pct"), ("cfar2d_rank_pct", 0xFFFFFFFF, b"rank_pct"),
     ("cfar2d_ref_range", 1 << 30, b"extents"),
     ("compat_rtl", 4, b"compat_rtl"), ("compat_rtl", 2, b"compat MTI"),   # MTI compat needs MTI on
-    ("range_shift", 14, b"range_shift"), ("spectrum_dtype", 2, b"spectrum_dtype"),
+    ("range_shift", 14, b"range_shift"), ("spectrum_dtype", 3, b"spectrum_dtype"),
 ])
 def test_create_rejects_bad_config(lib_built, field, value, msg):
     cfg = L.default_config()
@@ -214,3 +214,17 @@ def test_comm_check_verdict(lib_built):
     assert lib_built.fmcw_comm_check_decide_for_test(differ, 0, 32) == L.FMCW_EINVAL
     assert lib_built.fmcw_comm_check_decide_for_test(None, 0, 16) == L.FMCW_EINVAL
     assert lib_built.fmcw_comm_fail_next_alloc_for_test(0) == L.FMCW_OK
+
+
+@pytest.mark.parametrize("field,value", [("n_range", 2048), ("n_range", 8192), ("n_doppler", 32),
+                                         ("mti_mode", 2)])
+def test_s48_spectrum_limits(lib_built, field, value):
+    """FMCW_SPEC_S48 shares an exponent over 4 chirps of a K1 tile row and a K2 lane quad:
+    n_range <= 1024, n_doppler >= 64, MTI off, fp32 window -- rejected at fmcw_create otherwise."""
+    cfg = L.default_config()
+    cfg.spectrum_dtype = L.SPEC_S48
+    setattr(cfg, field, value)
+    h = C.c_void_p()
+    assert lib_built.fmcw_create(C.byref(cfg), C.byref(h)) == L.FMCW_EINVAL
+    assert b"S48" in lib_built.fmcw_last_error()
+    assert not h.value
