@@ -157,7 +157,7 @@ constexpr size_t cfar2d_smem_bytes(int hr) {
 #define FMCW_K3_LV_QB 680
 #endif
 #ifndef K3_SCREEN_AHEAD  // rows of the level screen's LDS reads in flight ahead of the accumulation
-#define K3_SCREEN_AHEAD 3
+#define K3_SCREEN_AHEAD 2
 #endif
 // level nibbles of 4 cells from their key16 pairs (cells d, d + 1 | d + 2, d + 3): (k | 0x8000) - Q has
 // bit 15 set iff k >= Q (k < 0x8000, 1 <= Q <= 0x8000: no borrow across the halves); the byte
@@ -792,6 +792,450 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
         }
       }
     }  // steps
+  }    // strips
+}
+
+// ---- K3a for the reference window (HD 6, GD 2, compile-time HR / GR; round 5): the level screen
+// with the scale rules, and no candidate test inside the launch -- its survivors go straight to
+// K3b's exact decision.
+//
+// Round 4's screen ruled a cell out only at the smallest scale s_min (= sc_min 2): with Rayleigh
+// clutter 1.6 % of the cells (config 5) have cut >= 2 x the 68 % level, and a candidate test on LDS
+// keys (~40 % of the launch) sorted them out again.  A cell gets sc_min only when #{ref < mean / 2}
+// >= rank + 1 (os_cfar_2d.vhd:195-199).  If C_Q refs lie at or above a level q = lo(Q) and the mean
+// is at most 2 q, those C_Q >= need refs are not below mean / 2, so at most rank refs are: the
+// scale is >= s2 = min(sc_nom, sc_max), and E(s2) >= C_Q >= need rules the cell out when cut <
+// fl(s2 q), i.e. key16(cut) < U2 = key16(fl(s2 q)).  The mean is bounded from counts at two more
+// levels per strip, C = QB + 1 octave (2 b) and D = QB + 2 octaves (4 b), b = lo(QB), a = lo(QA):
+// with no cell of the 11 x 13 box at or above D, every ref is < a, < b, < 2 b or < 4 b by its level, so
+//   rule B: sum < b (n + C_B + 2 C_C)            <= 255 b   when C_B <= 63, C_C <= 32
+//   rule A: sum < a (n + (b/a - 1) C_A + (b/a) C_B + 2 (b/a) C_C)
+//                                                <= 252 a   when b <= 1.5 a, C_A <= 80, C_B <= 40, C_C <= 8
+// (n = 128; C_A / C_B count refs, C_C / C_D the whole box), and the fp32 tree mean then stays below
+// 2 q (the tree sum of 128 non-negative terms is within 2^-21 of the sum).  RTL-compat cells: the
+// integer mean floor(sum / n) >> 1 is below the same bound.  NumPy model on the bench's maps
+// (tools/k3_screen_model.py --rules): survivors 1.60 % -> 0.033 % (config 5), 0.014 % -> 0.009 %
+// (config 3).
+//
+// LDS per ring row: two nibble-seed rows (bit 0 / bit 4 of a byte: key16 >= QA / QB, and >= QC /
+// QD) with circular halos, and a cut-code row (a nibble per cell: key16 < UA, UB, U2A, U2B) --
+// 2.5 B per cell instead of round 4's 3 B (key16 + one seed row), so config 5 fits 4 workgroups per
+// CU (39.3 KB each).  Every rule is exact in its own right; a cell that passes none of them goes to
+// K3b (key16(cut) is an upper bound: the rules only ever keep more cells).
+template <int NC, int HR, int GR> struct LvGeom {
+  static constexpr int NT = 256, WPB = 4, WR = DopplerGeom<NC>::WR, TR = WPB * WR, TPR = NC / 16;
+  static constexpr int RB = NC + 2 * MH + 16;   // seed row stride (bytes; b7idx layout, circular halos)
+  static constexpr int CS = NC / 2;             // cut-code row (a nibble per cell, no halos)
+  static constexpr int NR = TR + 2 * HR;        // ring rows
+  static constexpr int N_REF = (2 * HR + 1) * 13 - (2 * GR + 1) * 5;
+  static constexpr int HIST = 128 + 16;         // u32: level histogram + counters
+  static constexpr int CAPB = 256, CAPT = 128;  // strip buffer: survivor cells, (tile, run) pairs
+  static constexpr size_t SMEM = (size_t)NR * (2 * RB + CS) + (HIST + CAPB + 2 * CAPT) * 4;
+  static_assert(RB % 16 == 0 && CS % 8 == 0 && TR * NC == 16 * NT, "a step's rows are 16 cells per thread");
+};
+
+template <int NC, int HR, int GR>
+constexpr size_t cfar2d_lv_smem_bytes() { return LvGeom<NC, HR, GR>::SMEM; }
+
+// The four cut-code flags of 4 cells (kw: their key16 pairs) as a 16-bit word of nibbles (cell j in
+// bits 4j .. 4j + 3; bit k = key16 < U_k, W_k = (U_k | 0x8000) - 1 in both halves, as
+// cfar2d_screen_lv's CUT side)
+__device__ __forceinline__ uint32_t lv_cut_code(uint2 kw, const uint32_t (&W)[4]) {
+  uint32_t n = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t f = __builtin_amdgcn_perm(W[k] - kw.y, W[k] - kw.x, 0x07050301u);  // bit 7 of byte j
+    n |= (f >> (7 - k)) & (0x01010101u << k);
+  }
+  const uint32_t t = n | (n >> 4);        // byte 0 = cells 0, 1; byte 2 = cells 2, 3
+  return (t & 0xffu) | ((t >> 8) & 0xff00u);
+}
+
+// Survivor bits (bit j: cell d0 + j may detect) of this lane's 16 CUTs, CUT row rl of the group tile.
+template <int NC, int HR, int GR>
+__device__ __forceinline__ uint32_t cfar2d_screen_rules(const uint8_t* ab, const uint8_t* cd, const uint8_t* code,
+                                                        int base, int rl, int d0, int need, bool ruleA) {
+  using Gm = LvGeom<NC, HR, GR>;
+  constexpr int NR = Gm::NR, RB = Gm::RB, CS = Gm::CS, NW = 2 * HR + 1;
+  static_assert(Gm::N_REF == 128 && 2 * HR + 1 <= 15 && 5 * (2 * GR + 1) <= 15, "thresholds below are for n_ref 128");
+  // column sums: V (seeds A/B) over the window rows, G over the guard rows, W (seeds C/D) over the box;
+  // a rolling window of K3_SCREEN_AHEAD rows of LDS reads in flight (sched_barrier + opaque sums)
+  uint32_t V[8], G[6], W[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) V[k] = W[k] = 0u;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) G[k] = 0u;
+  constexpr int AH = K3_SCREEN_AHEAD < NW ? K3_SCREEN_AHEAD : NW;
+  int sl = rl + base;
+  sl = sl >= NR ? sl - NR : sl;
+  uint4 qa[AH], qb[AH], qc[AH], qd[AH];
+  auto load_row = [&](int j) {
+    const uint8_t* pa = ab + sl * RB + b7idx(d0 - 8);
+    const uint8_t* pc = cd + sl * RB + b7idx(d0 - 8);
+    qa[j % AH] = *reinterpret_cast<const uint4*>(pa);
+    qb[j % AH] = *reinterpret_cast<const uint4*>(pa + 16);
+    qc[j % AH] = *reinterpret_cast<const uint4*>(pc);
+    qd[j % AH] = *reinterpret_cast<const uint4*>(pc + 16);
+    sl = sl + 1 == NR ? 0 : sl + 1;
+  };
+#pragma unroll
+  for (int j = 0; j < AH; ++j) load_row(j);
+#pragma unroll
+  for (int j = 0; j < NW; ++j) {
+    const int dr = j - HR;
+    __builtin_amdgcn_sched_barrier(0);
+    const uint4 a0 = qa[j % AH], a1 = qb[j % AH], c0 = qc[j % AH], c1 = qd[j % AH];
+    const uint32_t D[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const uint32_t E[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    if (j + AH < NW) load_row(j + AH);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      V[k] += D[k];
+      W[k] += E[k];
+    }
+    if (dr >= -GR && dr <= GR) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) G[k] += D[k + 1];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(V[k]), "+v"(W[k]));
+#pragma unroll
+    for (int k = 0; k < 6; ++k) asm volatile("" : "+v"(G[k]));
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // 13-cell window sums per level (bytes: cell d0 + 4m + t in word m byte t)
+  uint32_t HA[4], HB[4], HC[4], HD[4];
+  {
+    uint32_t XA[7], XB[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const uint32_t w = __builtin_amdgcn_alignbyte(V[k + 1], V[k], 2);
+      XA[k] = w & 0x0F0F0F0Fu;
+      XB[k] = (w >> 4) & 0x0F0F0F0Fu;
+    }
+    lv_sum13(XA, HA);
+    lv_sum13(XB, HB);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const uint32_t w = __builtin_amdgcn_alignbyte(W[k + 1], W[k], 2);
+      XA[k] = w & 0x0F0F0F0Fu;
+      XB[k] = (w >> 4) & 0x0F0F0F0Fu;
+    }
+    lv_sum13(XA, HC);
+    lv_sum13(XB, HD);
+  }
+  // guard block (3 x 5 around the CUT) of seeds A / B in the nibbles
+  uint32_t H5[4];
+  {
+    uint32_t Gp[5], S2[5], S4[4];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) Gp[k] = __builtin_amdgcn_alignbyte(G[k + 1], G[k], 2);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) S2[k] = Gp[k] + __builtin_amdgcn_alignbyte(k < 4 ? Gp[k + 1] : 0u, Gp[k], 1);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) S4[k] = S2[k] + __builtin_amdgcn_alignbyte(S2[k + 1], S2[k], 2);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) H5[m] = S4[m] + Gp[m + 1];
+  }
+  // the 16 CUTs' code nibbles (cells d0 .. d0 + 15 of the CUT row)
+  int cs = rl + HR + base;
+  cs = cs >= NR ? cs - NR : cs;
+  const uint2 cw = *reinterpret_cast<const uint2*>(code + cs * CS + d0 / 2);
+  constexpr uint32_t H = 0x80808080u;
+  auto K = [](int v) { return (uint32_t)v * 0x01010101u; };
+  const uint32_t k_need = K(128 - need);
+  uint32_t bits = 0;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const uint32_t h16 = ((m < 2 ? cw.x : cw.y) >> (16 * (m & 1))) & 0xffffu;
+    const uint32_t e = __builtin_amdgcn_perm(h16, h16, 0x01010000u);       // bytes lo, lo, hi, hi
+    const uint32_t nb = (e & 0x000f000fu) | ((e >> 4) & 0x0f000f00u);      // byte t: cell 4m + t's code
+    const uint32_t CA = HA[m] - (H5[m] & 0x0F0F0F0Fu), CB = HB[m] - ((H5[m] >> 4) & 0x0F0F0F0Fu);
+    const uint32_t CC = HC[m], CD = HD[m];
+    const uint32_t na = CA + k_need, nb2 = CB + k_need;                     // bit 7: C_A / C_B >= need
+    const uint32_t smin = (na & (nb << 7)) | (nb2 & (nb << 6));             // E(s_min) >= need at A or B
+    const uint32_t nzD = ((CD & 0x7f7f7f7fu) + 0x7f7f7f7fu) | CD;           // bit 7: C_D != 0
+    const uint32_t rB = nb2 & ~(CB + K(64)) & ~(CC + K(95)) & ~nzD & (nb << 4);
+    uint32_t rA = na & ~(CA + K(47)) & ~(CB + K(87)) & ~((CC & 0x7f7f7f7fu) + K(119)) & ~nzD & (nb << 5);
+    if (!ruleA) rA = 0u;
+    const uint32_t surv = ~(smin | rA | rB) & H;
+    bits |= ((surv * 0x00204081u) >> 28) << (4 * m);  // bit 7 of byte t -> bit 28 + t
+  }
+  return bits;
+}
+
+template <int NC, int HR, int GR>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int frame0, int tile0, Cfar2DArgs a,
+            DetSink sink, Cfar2Cands cands) {
+  (void)frame0;
+  using Gm = LvGeom<NC, HR, GR>;
+  constexpr int WR = Gm::WR, NT = Gm::NT, RB = Gm::RB, CS = Gm::CS, TPR = Gm::TPR, WPB = Gm::WPB, TR = Gm::TR;
+  constexpr int NR = Gm::NR;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem8[];
+  uint8_t* const ab = smem8;
+  uint8_t* const cd = ab + NR * RB;
+  uint8_t* const code = cd + NR * RB;
+  uint32_t* const hist = reinterpret_cast<uint32_t*>(code + NR * CS);
+  uint32_t* const cnt = hist + 128;    // [0..3] wave counts, [4] / [5] buffer fill, [6] / [7] flush bases
+  uint32_t* const buf = cnt + 16;      // the strip's survivor cells (Gm::CAPB)
+  uint32_t* const bt = buf + Gm::CAPB; // their wave tiles: (tile, offset << 16 | count) (Gm::CAPT)
+  constexpr int CAPB = Gm::CAPB, CAPT = Gm::CAPT;
+  // The candidate list takes a strip's survivors in one reservation (two atomics per flush): an
+  // atomic per wave tile on the launch's two counters -- every workgroup on the same two words --
+  // cost ~0.5 ms per launch with ~10^5 survivors (config 5, measured).
+  auto flush = [&]() {  // uniform; every thread of the workgroup calls it
+    const uint32_t n = cnt[4], m = cnt[5];
+    if (n == 0u) return;
+    __syncthreads();  // every thread has read cnt[4], cnt[5]
+    if (threadIdx.x == 0) {
+      cnt[6] = atomicAdd(&cands.ctr[0], n);
+      cnt[7] = atomicAdd(&cands.ctr[1], m);
+      cnt[4] = cnt[5] = 0u;
+    }
+    __syncthreads();
+    const uint32_t p0 = cnt[6], q0 = cnt[7];
+    for (uint32_t i = threadIdx.x; i < n; i += NT) cands.cell[p0 + i] = buf[i];
+    for (uint32_t j = threadIdx.x; j < m; j += NT) {
+      const uint32_t wt = bt[2 * j], oc = bt[2 * j + 1];
+      cands.tiles[q0 + j] = wt;
+      sink.wg_base[wt] = p0 + (oc >> 16);
+      sink.wg_count[wt] = oc & 0xffffu;
+    }
+    __syncthreads();  // the buffer is free again
+  };
+  if (threadIdx.x == 0) cnt[4] = cnt[5] = 0u;
+
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int need = a.n_ref - a.rank;
+  const int wt_per_frame = ns / WR;
+  const int wg_per_frame = (wt_per_frame + WPB - 1) / WPB;
+  const int spf = (wg_per_frame + steps - 1) / steps;
+  const int nf = n_strips / spf;
+  const int tid = opaque(threadIdx.x);
+  // a TR-row block of cells (4096) as 4 float4 per thread, lanes contiguous per load: float4 e4 =
+  // tid + u NT is row e4 / (NC / 4), cells 4 (e4 % (NC / 4)) .. + 3
+  auto blk = [](int u, int& i, int& d) {  // recomputed at each use (not held across the step)
+    const int e4 = opaque(threadIdx.x) + u * NT;
+    i = e4 / (NC / 4);
+    d = (e4 - i * (NC / 4)) * 4;
+  };
+
+  // per strip: level words (seed rows) and cut-code thresholds
+  uint32_t qa2 = 0, qb2 = 0, qc2 = 0, qd2 = 0;
+  uint32_t Wc[4] = {0, 0, 0, 0};
+  bool ruleA = false;
+  auto put = [&](int x, int d, float4 v) {  // ring row x (0 = the step's first halo row), cells d .. d + 3
+    v = a.compat ? q17x4(v) : nonneg4(v);
+    const uint2 kw = make_uint2(key16(v.x) | (key16(v.y) << 16), key16(v.z) | (key16(v.w) << 16));
+    const uint32_t wab = lv_nibbles(kw, qa2, qb2), wcd = lv_nibbles(kw, qc2, qd2);
+    uint8_t* ra = ab + x * RB;
+    uint8_t* rc = cd + x * RB;
+    *reinterpret_cast<uint32_t*>(ra + b7idx(d)) = wab;
+    *reinterpret_cast<uint32_t*>(rc + b7idx(d)) = wcd;
+    if (d < MH) {
+      *reinterpret_cast<uint32_t*>(ra + b7idx(NC + d)) = wab;
+      *reinterpret_cast<uint32_t*>(rc + b7idx(NC + d)) = wcd;
+    }
+    if (d >= NC - MH) {
+      *reinterpret_cast<uint32_t*>(ra + b7idx(d - NC)) = wab;
+      *reinterpret_cast<uint32_t*>(rc + b7idx(d - NC)) = wcd;
+    }
+    *reinterpret_cast<uint16_t*>(code + x * CS + d / 2) = (uint16_t)lv_cut_code(kw, Wc);
+  };
+
+  for (int g = blockIdx.x; g < n_strips; g += gridDim.x) {
+    const int f = g % nf;
+    const int t_beg = (g / nf) * steps, t_end = min(t_beg + steps, wg_per_frame);
+    const float* fm = map + (size_t)f * ns * NC;
+    int base = 0;  // ring slot of tile row 0
+    float4 pre[4];
+    for (int t = t_beg; t < t_end; ++t) {
+      const int wt0 = t * WPB;
+      const int n_wt = min(WPB, wt_per_frame - wt0);
+      const int r0 = wt0 * WR;
+      const int rlw = wv * WR + lane / TPR;
+      const int d0 = (lane % TPR) * 16;
+      const int r = r0 + rlw;
+      __syncthreads();  // the previous step's waves are done with the rows
+      if (t == t_beg) {
+        // levels: the mean key7 level of the first step's CUT rows (this thread's 16 cells), then the
+        // FMCW_K3_LV_QA / _QB quantiles of a 128-bin histogram around it
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          int i, d;
+          blk(u, i, d);
+          v[u] = r0 + i < ns ? *reinterpret_cast<const float4*>(fm + (size_t)(r0 + i) * NC + d)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if (threadIdx.x == 0) cnt[12] = 0u;
+        if (threadIdx.x < 128) hist[threadIdx.x] = 0u;
+        uint32_t k7[16];
+        uint32_t sum = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float4 w = a.compat ? q17x4(v[u]) : nonneg4(v[u]);
+          k7[4 * u] = key16(w.x) >> 3;
+          k7[4 * u + 1] = key16(w.y) >> 3;
+          k7[4 * u + 2] = key16(w.z) >> 3;
+          k7[4 * u + 3] = key16(w.w) >> 3;
+          sum += k7[4 * u] + k7[4 * u + 1] + k7[4 * u + 2] + k7[4 * u + 3];
+        }
+#pragma unroll
+        for (int x = 32; x >= 1; x >>= 1) sum += (uint32_t)__shfl_xor((int)sum, x, 64);
+        __syncthreads();  // counters zeroed
+        if (lane == 0) atomicAdd(&cnt[12], sum);
+        __syncthreads();
+        const int mean7 = (int)(cnt[12] / (uint32_t)(TR * NC));
+        const int h0 = mean7 - 64;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) atomicAdd(&hist[min(max((int)k7[i] - h0, 0), 127)], 1u);
+        __syncthreads();
+        if (wv == 0) {
+          const uint32_t c0 = hist[2 * lane], c1 = hist[2 * lane + 1];
+          int tot;
+          const uint32_t ex = (uint32_t)wave_excl_scan((int)(c0 + c1), tot);
+          const uint32_t cum0 = ex + c0, cum1 = ex + c0 + c1;
+          const uint32_t na = (uint32_t)(FMCW_K3_LV_QA * (TR * NC) / 1000), nb = (uint32_t)(FMCW_K3_LV_QB * (TR * NC) / 1000);
+          const uint64_t ba0 = __ballot(cum0 >= na), ba1 = __ballot(cum1 >= na);
+          const uint64_t bb0 = __ballot(cum0 >= nb), bb1 = __ballot(cum1 >= nb);
+          auto first_bin = [](uint64_t m0, uint64_t m1) {
+            const int l = __builtin_ctzll(m1);
+            return (m0 >> l) & 1u ? 2 * l : 2 * l + 1;
+          };
+          if (lane == 0) {
+            cnt[14] = (uint32_t)first_bin(ba0, ba1);
+            cnt[15] = (uint32_t)first_bin(bb0, bb1);
+          }
+        }
+        __syncthreads();
+        const uint32_t QA = (uint32_t)min(max((h0 + (int)cnt[14]) * 8, 1), 0x7f80);
+        const uint32_t QB = (uint32_t)min(max((h0 + (int)cnt[15]) * 8, 1), 0x7f80);
+        // C / D one and two octaves above QB (exact: key16 + 128 doubles lo); the scale rules need them
+        // inside the finite range and no scale override
+        const bool s2ok = !a.override_ && QB + 256u < 0x7f80u;
+        const uint32_t QC = min(QB + 128u, 0x7f80u), QD = min(QB + 256u, 0x7f80u);
+        qa2 = QA | (QA << 16);
+        qb2 = QB | (QB << 16);
+        qc2 = QC | (QC << 16);
+        qd2 = QD | (QD << 16);
+        const float s2 = fminf(a.sc_nom, a.sc_max);
+        const uint32_t UA = key16(a.s_min * key_lo(QA)), UB = key16(a.s_min * key_lo(QB));
+        const uint32_t U2A = s2ok ? key16(s2 * key_lo(QA)) : 0u, U2B = s2ok ? key16(s2 * key_lo(QB)) : 0u;
+        ruleA = s2ok && key_lo(QB) <= 1.5f * key_lo(QA);
+        const uint32_t U[4] = {UA, UB, U2A, U2B};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) Wc[k] = ((U[k] | 0x8000u) - 1u) * 0x00010001u;
+        // the whole ring: rows r0 - hr .. r0 + TR + hr - 1 (zero outside the map), 4 float4 in flight
+        base = 0;
+        constexpr int n4 = NR * (NC / 4);
+        for (int b = tid; b < n4; b += 4 * NT) {
+          float4 w[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int e4 = b + u * NT;
+            const int x = e4 / (NC / 4), d = (e4 - x * (NC / 4)) * 4;
+            const int rr = r0 - HR + x;
+            w[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (e4 < n4 && rr >= 0 && rr < ns) w[u] = *reinterpret_cast<const float4*>(fm + (size_t)rr * NC + d);
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int e4 = b + u * NT;
+            const int x = e4 / (NC / 4), d = (e4 - x * (NC / 4)) * 4;
+            if (e4 < n4) put(x, d, w[u]);
+          }
+        }
+      } else {
+        // the ring turns by TR rows; the TR new rows (prefetched) go into the slots of the rows that left
+        base += TR;
+        if (base >= NR) base -= NR;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          int i, d;
+          blk(u, i, d);
+          int x = NR - TR + i + base;
+          x = x >= NR ? x - NR : x;
+          put(x, d, pre[u]);
+        }
+      }
+      if (t + 1 < t_end) {  // prefetch the next step's new rows r0 + TR + hr .. (zero past the map)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          int i, d;
+          blk(u, i, d);
+          const int rr = r0 + TR + HR + i;
+          pre[u] = rr < ns ? *reinterpret_cast<const float4*>(fm + (size_t)rr * NC + d) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+      __syncthreads();
+      const bool has_tile = wv < n_wt;
+      uint32_t surv = 0;
+      if (has_tile && r >= HR && r < ns - HR) surv = cfar2d_screen_rules<NC, HR, GR>(ab, cd, code, base, rlw, d0, need, ruleA);
+#ifdef FMCW_K3_COUNT  // lab builds (tools/cfar2d_bench.py FMCW_K3_COUNTS=1): survivors into sink.counter[2]
+      {
+        int s1 = __popc(surv);
+        for (int o = 32; o >= 1; o >>= 1) s1 += __shfl_xor(s1, o, 64);
+        if (lane == 0) atomicAdd(&sink.counter[2], (uint32_t)s1);
+      }
+#endif
+      // emission: each wave tile's survivors, in (range, doppler) order, as one run of the strip
+      // buffer (flushed to the candidate list when full and at the strip's end); an empty tile is
+      // final here.  (wg_base, wg_count) = (run start, run length) until k_cfar2d_emit.
+      const int wtile = tile0 + f * wt_per_frame + wt0 + wv;
+      int k_w = 0;
+      const int ex = wave_excl_scan(has_tile ? __popc(surv) : 0, k_w);
+      if (lane == 0) cnt[wv] = (uint32_t)k_w;
+      if (has_tile && k_w == 0 && lane == 0) {
+        sink.wg_base[wtile] = (uint32_t)wtile * sink.slot_cap;
+        sink.wg_count[wtile] = 0u;
+      }
+      __syncthreads();
+      uint32_t T = 0, woff = 0, ti = 0, nt = 0;
+#pragma unroll
+      for (int i = 0; i < WPB; ++i) {
+        const uint32_t c = cnt[i];
+        woff += i < wv ? c : 0u;
+        ti += (i < wv && c) ? 1u : 0u;
+        T += c;
+        nt += c ? 1u : 0u;
+      }
+      if (T != 0u) {  // uniform
+        if (cnt[4] + T > (uint32_t)CAPB || cnt[5] + nt > (uint32_t)CAPT) flush();
+        const uint32_t bn = cnt[4], tn = cnt[5];
+        const uint32_t cbase = ((uint32_t)f * (uint32_t)ns + (uint32_t)r) * (uint32_t)NC + (uint32_t)d0;
+        if (T > (uint32_t)CAPB) {  // a dense step: its own reservation, one per wave tile
+          if (k_w) {
+            uint32_t p0 = 0u;
+            if (lane == 0) {
+              p0 = atomicAdd(&cands.ctr[0], (uint32_t)k_w);
+              cands.tiles[atomicAdd(&cands.ctr[1], 1u)] = (uint32_t)wtile;
+              sink.wg_base[wtile] = p0;
+              sink.wg_count[wtile] = (uint32_t)k_w;
+            }
+            p0 = (uint32_t)__shfl((int)p0, 0, 64);
+            uint32_t o = p0 + (uint32_t)ex;
+            for (uint32_t m = surv; m; m &= m - 1, ++o) cands.cell[o] = cbase + (uint32_t)__builtin_ctz(m);
+          }
+        } else if (k_w) {
+          uint32_t o = bn + woff + (uint32_t)ex;
+          for (uint32_t m = surv; m; m &= m - 1, ++o) buf[o] = cbase + (uint32_t)__builtin_ctz(m);
+          if (lane == 0) {
+            bt[2 * (tn + ti)] = (uint32_t)wtile;
+            bt[2 * (tn + ti) + 1] = ((bn + woff) << 16) | (uint32_t)k_w;
+          }
+        }
+        __syncthreads();  // every thread has read cnt[0 .. 5]
+        if (threadIdx.x == 0 && T <= (uint32_t)CAPB) {
+          cnt[4] = bn + T;
+          cnt[5] = tn + nt;
+        }
+      }
+    }  // steps
+    __syncthreads();
+    flush();  // the strip's last runs
   }    // strips
 }
 

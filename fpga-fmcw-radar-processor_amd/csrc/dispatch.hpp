@@ -54,12 +54,12 @@ using Cfar2Fn = void (*)(const float*, int, int, int, int, int, Cfar2DArgs, DetS
 using Cfar2DecideFn = void (*)(const float*, int, Cfar2DArgs, Cfar2Cands);
 using Cfar2EmitFn = void (*)(const float*, int, int, Cfar2DArgs, Cfar2Cands, DetSink);
 struct Cfar2Info {
-  Cfar2Fn fn;           // K3a k_cfar2d: screen, candidate test, the candidate list
+  Cfar2Fn fn;           // K3a k_cfar2d_lv (reference window) / k_cfar2d (any other): screen, the candidate list
   int TR;
   Cfar2DecideFn decide; // K3b k_cfar2d_decide
   Cfar2EmitFn emit;     // K3c k_cfar2d_emit
+  size_t smem;          // K3a's dynamic LDS bytes
 };
 Cfar2Info cfar2_info(uint32_t nc, int hd, int gd, int hr, int gr);  // inst_cfar2.hip
-size_t cfar2_smem(uint32_t nc, int hr);
 
 }  // namespace fmcw

@@ -380,7 +380,7 @@ int validate(const fmcw_config& c) {
       return fail(FMCW_EINVAL, "2-D CFAR window wider than n_doppler");
     if (c.cfar2d_scale_override > 7)
       return fail(FMCW_EINVAL, "scale_override is a 3-bit port (0..7)");
-    if (cfar2_smem(c.n_doppler, a.hr) > 160 * 1024)
+    if (cfar2_info(c.n_doppler, a.hd, a.gd, a.hr, a.gr).smem > 160 * 1024)
       return fail(FMCW_EINVAL, "2-D CFAR range extent too large for LDS");
   } else if (c.cfar_kind != FMCW_CFAR_NONE) {
     return fail(FMCW_EINVAL, "cfar_kind=%d unknown", c.cfar_kind);
@@ -560,10 +560,10 @@ int arm_counters(fmcw_handle* h, hipStream_t s, bool cap) {
 
 constexpr size_t kCfar2Batch = 16;  // frames per 2-D CFAR launch on the caller's map (at least)
 #ifndef FMCW_K3_DECIDE_GRID
-#define FMCW_K3_DECIDE_GRID 1024
+#define FMCW_K3_DECIDE_GRID 2048
 #endif
 #ifndef FMCW_K3_EMIT_GRID
-#define FMCW_K3_EMIT_GRID 256
+#define FMCW_K3_EMIT_GRID 1024
 #endif
 constexpr int kCfar2DecideGrid = FMCW_K3_DECIDE_GRID;  // K3b workgroups (4 waves each, one candidate per wave at a time)
 constexpr int kCfar2EmitGrid = FMCW_K3_EMIT_GRID;      // K3c workgroups (one wave tile per wave at a time)
@@ -849,8 +849,8 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   }
   if (c.cfar_kind == FMCW_CFAR_OS2D) {
     const Cfar2DArgs a = cfar2_args(c);
-    h->cfar2d_smem = cfar2_smem(c.n_doppler, a.hr);
     const Cfar2Info ci = cfar2_info(c.n_doppler, a.hd, a.gd, a.hr, a.gr);  // the kernel launch_cfar runs
+    h->cfar2d_smem = ci.smem;
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(ci.fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)h->cfar2d_smem) != hipSuccess)
       (void)hipGetLastError();

@@ -3,33 +3,35 @@
 
 namespace fmcw {
 
-// the reference window (range half extent 5, guard 1; Doppler half extent 6, guard 2: os_cfar_2d
-// as instantiated at radar_core.vhd:376-382) gets the compile-time level screen; any other
-// geometry the generic kernel (runtime window, pair screen)
+// The reference window (range half extent 5, guard 1; Doppler half extent 6, guard 2: os_cfar_2d
+// as instantiated at radar_core.vhd:376-382) gets a level screen; any other geometry the generic
+// kernel (runtime window, pair screen, candidate test).  Of the two level-screen kernels, k_cfar2d
+// (key16 rows + in-launch candidate test) runs where its ring fits 4 workgroups per CU (<= 40 KB of
+// LDS: NC <= 512), k_cfar2d_lv (scale rules, 2.5 B per cell, no candidate test) where it does not
+// (NC = 1024: 46.7 KB, 3 workgroups per CU).  Measured (tools/cfar2d_bench.py, 16 frames, us per
+// launch, profiles/r05/k3_rules/): config 5 k_cfar2d 350, k_cfar2d_lv 297-302; config 3 k_cfar2d
+// 73, k_cfar2d_lv 95-100 (its 4-rx NCI cells pass the s_min screen rarely: the rules' extra screen
+// work buys nothing there).
+static bool lv_window(int hd, int gd, int hr, int gr) { return hd == 6 && gd == 2 && hr == 5 && gr == 1; }
 template <int N>
-static Cfar2Fn cfar2_fn(int hd, int gd, int hr, int gr) {
-  return (hd == 6 && gd == 2 && hr == 5 && gr == 1) ? k_cfar2d<N, 6, 2, 5, 1> : k_cfar2d<N, 0, 0>;
+constexpr bool rules_kernel() { return cfar2d_smem_bytes<N>(5) > 40 * 1024; }
+
+template <int N>
+static Cfar2Info info_t(bool lv, int hr) {
+  constexpr bool R = rules_kernel<N>();
+  Cfar2Fn fn = !lv ? k_cfar2d<N, 0, 0> : R ? k_cfar2d_lv<N, 5, 1> : k_cfar2d<N, 6, 2, 5, 1>;
+  const size_t smem = !lv ? cfar2d_smem_bytes<N>(hr) : R ? cfar2d_lv_smem_bytes<N, 5, 1>() : cfar2d_smem_bytes<N>(5);
+  return {fn, Cfar2DGeom<N>::TR, k_cfar2d_decide<N>, k_cfar2d_emit<N>, smem};
 }
 
 Cfar2Info cfar2_info(uint32_t nc, int hd, int gd, int hr, int gr) {
+  const bool lv = lv_window(hd, gd, hr, gr);
   switch (nc) {
-#define C_(N) case N: return {cfar2_fn<N>(hd, gd, hr, gr), Cfar2DGeom<N>::TR, k_cfar2d_decide<N>, k_cfar2d_emit<N>};
+#define C_(N) case N: return info_t<N>(lv, hr);
     C_(32) C_(64) C_(128) C_(256) C_(512) C_(1024)
 #undef C_
   }
-  return {nullptr, 0};
-}
-
-size_t cfar2_smem(uint32_t nc, int hr) {
-  switch (nc) {
-    case 32: return cfar2d_smem_bytes<32>(hr);
-    case 64: return cfar2d_smem_bytes<64>(hr);
-    case 128: return cfar2d_smem_bytes<128>(hr);
-    case 256: return cfar2d_smem_bytes<256>(hr);
-    case 512: return cfar2d_smem_bytes<512>(hr);
-    case 1024: return cfar2d_smem_bytes<1024>(hr);
-  }
-  return 0;
+  return {nullptr, 0, nullptr, nullptr, 0};
 }
 
 }  // namespace fmcw
