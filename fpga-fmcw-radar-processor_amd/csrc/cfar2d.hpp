@@ -48,27 +48,22 @@ struct Cfar2Cands {
 // 7-bit keys.  key(v) = clamp((bits(v) >> SH) - base, 0, 127) for a non-negative fp32 cell v:
 // 2^(23 - SH) levels per octave (16 at SH = 19) over a 128-level window that starts `base`
 // levels up; base is set per strip from the mean level of its first step's cells minus LOW
-// (FMCW_K3_KEY_LOW, 64: the window spans 4 octaves below the mean level to 4 above, where
+// (kK3KeyLow, 64: the window spans 4 octaves below the mean level to 4 above, where
 // Rayleigh noise and the cut / s_min levels it is tested against lie).  The key is monotone
 // non-decreasing in v, with clamping at both ends, and NaN maps to 0 (a NaN reference never
 // counts), so key(ref) > key(q) implies ref > q.  Cells above the window all get 127: they
 // count as references, and as CUTs they are never screened out (no key is above 127).
-#ifndef FMCW_K3_KEY_SHIFT
-#define FMCW_K3_KEY_SHIFT 19
-#endif
-#ifndef FMCW_K3_KEY_LOW
-#define FMCW_K3_KEY_LOW 64
-#endif
+constexpr int kK3KeyShift = 19, kK3KeyLow = 64;
 __device__ __forceinline__ uint32_t key7(float v, int base) {
   const uint32_t b = __float_as_uint(v);
-  const int k = b > 0x7f800000u ? -1 : (int)(b >> FMCW_K3_KEY_SHIFT) - base;
+  const int k = b > 0x7f800000u ? -1 : (int)(b >> kK3KeyShift) - base;
   return (uint32_t)min(max(k, 0), 127);
 }
 // key(q) + 1 for q = fl(c * inv_s) + 8 ulps (c * fl(1 / s): <= 2 ulps of error), c = the CUT:
 // a pair max whose key is >= this has max > q > c / s in reals, so fl(s * max) >= c.
 // (No NaN test: a NaN cut gets 128, which no key reaches, so the cell is never screened out.)
 __device__ __forceinline__ uint32_t cut_key7(float c, float inv_s, int base) {
-  const int k = (int)((__float_as_uint(c * inv_s) + 8u) >> FMCW_K3_KEY_SHIFT) - base;
+  const int k = (int)((__float_as_uint(c * inv_s) + 8u) >> kK3KeyShift) - base;
   return (uint32_t)min(max(k, 0), 127) + 1u;
 }
 
@@ -141,7 +136,7 @@ constexpr size_t cfar2d_smem_bytes(int hr) {
 // sliding row sums of those.  Every ref counted lies >= lo(Q), so fl(s_min r) >= P = fl(s_min lo(Q))
 // (rounding is monotone); a CUT with key16(cut) < U = key16(P) has cut < lo(U) <= P.  So
 // key16(cut) < U and count_Q >= need give E(s_min) >= need: the cell cannot detect at any scale
-// >= s_min.  Two levels A <= B per strip, at the FMCW_K3_LV_QA / _QB quantiles (56 % / 68 %) of
+// >= s_min.  Two levels A <= B per strip, at the kK3LvQA / _QB quantiles (56 % / 68 %) of
 // the key7 levels of the strip's first 4096 cells: a CUT is screened out if either level rules it
 // out.  Quantiles, not offsets from the mean, so the levels follow the clutter's spread (config 3's
 // 4-rx NCI cells are far narrower than config 5's Rayleigh ones).  Survivors on the bench maps
@@ -150,15 +145,10 @@ constexpr size_t cfar2d_smem_bytes(int hr) {
 // Ring rows hold per cell one byte: bit 0 = key >= QA, bit 4 = key >= QB, so both levels' column
 // sums (<= 2 HR + 1 <= 15) add in the nibbles of one 32-bit add; the 13-cell row sums (<= 143) of
 // each level are taken from byte prefix sums, the guard block's 5-cell sums (<= 15) in nibbles.
-#ifndef FMCW_K3_LV_QA  // the two levels: quantiles (per mille) of the strip's first-step cells
-#define FMCW_K3_LV_QA 560
-#endif
-#ifndef FMCW_K3_LV_QB
-#define FMCW_K3_LV_QB 680
-#endif
-#ifndef K3_SCREEN_AHEAD  // rows of the level screen's LDS reads in flight ahead of the accumulation
-#define K3_SCREEN_AHEAD 2
-#endif
+// the two levels: quantiles (per mille) of the strip's first-step cells; rows of the level
+// screen's LDS reads in flight ahead of the accumulation (round 5: 2 or 3 measured alike, 2 keeps
+// k_cfar2d_lv spill-free at 4 waves per SIMD)
+constexpr int kK3LvQA = 560, kK3LvQB = 680, kK3ScreenAhead = 2;
 // level nibbles of 4 cells from their key16 pairs (cells d, d + 1 | d + 2, d + 3): (k | 0x8000) - Q has
 // bit 15 set iff k >= Q (k < 0x8000, 1 <= Q <= 0x8000: no borrow across the halves); the byte
 // permute collects bits 15 / 31 of both words as bit 7 of 4 bytes
@@ -201,10 +191,10 @@ __device__ __forceinline__ uint32_t cfar2d_screen_lv(const RowRing& rr, int rl, 
   for (int k = 0; k < 8; ++k) V[k] = 0u;
 #pragma unroll
   for (int k = 0; k < 6; ++k) G[k] = 0u;
-  // The 2 HR + 1 rows' 32-byte windows, with at most K3_SCREEN_AHEAD rows' loads in flight: left to
+  // The 2 HR + 1 rows' 32-byte windows, with at most kK3ScreenAhead rows' loads in flight: left to
   // itself the scheduler issued all 22 LDS reads first (88 VGPRs of loads, the kernel's register
   // peak); the scheduling barriers keep a rolling window of loads ahead of the accumulation.
-  constexpr int NW = 2 * HR + 1, AH = K3_SCREEN_AHEAD < NW ? K3_SCREEN_AHEAD : NW;
+  constexpr int NW = 2 * HR + 1, AH = kK3ScreenAhead < NW ? kK3ScreenAhead : NW;
   int sl = rr.slot(rl);  // ring slot of window row dr = -HR, advanced with wrap
   uint4 q0[AH], q1[AH];
   auto load_row = [&](int j) {
@@ -218,7 +208,7 @@ __device__ __forceinline__ uint32_t cfar2d_screen_lv(const RowRing& rr, int rl, 
 #pragma unroll
   for (int j = 0; j < NW; ++j) {
     const int dr = j - HR;
-    if constexpr (K3_SCREEN_AHEAD < 2 * HR + 1) __builtin_amdgcn_sched_barrier(0);
+    if constexpr (kK3ScreenAhead < 2 * HR + 1) __builtin_amdgcn_sched_barrier(0);
     const uint4 a0 = q0[j % AH], a1 = q1[j % AH];
     const uint32_t D[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
     if (j + AH < NW) load_row(j + AH);
@@ -228,7 +218,7 @@ __device__ __forceinline__ uint32_t cfar2d_screen_lv(const RowRing& rr, int rl, 
 #pragma unroll
       for (int k = 0; k < 6; ++k) G[k] += D[k + 1];
     }
-    if constexpr (K3_SCREEN_AHEAD < 2 * HR + 1) {
+    if constexpr (kK3ScreenAhead < 2 * HR + 1) {
       // the row's sums now (no reassociation into one add tree after every load)
 #pragma unroll
       for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(V[k]));
@@ -236,7 +226,7 @@ __device__ __forceinline__ uint32_t cfar2d_screen_lv(const RowRing& rr, int rl, 
       for (int k = 0; k < 6; ++k) asm volatile("" : "+v"(G[k]));
     }
   }
-  if constexpr (K3_SCREEN_AHEAD < 2 * HR + 1) __builtin_amdgcn_sched_barrier(0);
+  if constexpr (kK3ScreenAhead < 2 * HR + 1) __builtin_amdgcn_sched_barrier(0);
   // 13-cell window per level: realign so that word k byte t = cell d0 - 6 + 4k + t, then unpack
   uint32_t HA[4], HB[4];
   {
@@ -465,14 +455,11 @@ __device__ __forceinline__ uint32_t wave_select_kth(uint32_t ka, uint32_t kb, ui
   return 0u;  // unreachable for k < #active
 }
 
-#ifndef FMCW_K3_WAVES  // waves per SIMD the register budget is cut for
-#define FMCW_K3_WAVES 4
-#endif
 
 // HD > 0: the reference window (HD 6, GD 2, compile-time HR / GR) with the level screen; HD == 0:
 // any window, runtime geometry, the pair screen on 7-bit keys (cfar2d_screen7_generic).
 template <int NC, int HD, int GD, int HR = 0, int GR = 0>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FMCW_K3_WAVES)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int frame0, int tile0, Cfar2DArgs a,
          DetSink sink, Cfar2Cands cands) {
   (void)frame0;
@@ -572,7 +559,7 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
         if (LV && threadIdx.x < 128) list[threadIdx.x] = 0u;
         __syncthreads();
         // the first step's CUT rows (TR x NC = 4096 cells; ring rows hr .. hr + TR - 1): their mean
-        // level key16 >> 3 (= bits >> 19: 16 levels per octave), then (LV) the FMCW_K3_LV_QA / _QB
+        // level key16 >> 3 (= bits >> 19: 16 levels per octave), then (LV) the kK3LvQA / _QB
         // quantiles of a 128-level histogram around that mean
         uint32_t k7[16];
         {
@@ -605,7 +592,7 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
             int tot;
             const uint32_t ex = (uint32_t)wave_excl_scan((int)(c0 + c1), tot);
             const uint32_t cum0 = ex + c0, cum1 = ex + c0 + c1;
-            const uint32_t na = (uint32_t)(FMCW_K3_LV_QA * (TR * NC) / 1000), nb = (uint32_t)(FMCW_K3_LV_QB * (TR * NC) / 1000);
+            const uint32_t na = (uint32_t)(kK3LvQA * (TR * NC) / 1000), nb = (uint32_t)(kK3LvQB * (TR * NC) / 1000);
             const uint64_t ba0 = __ballot(cum0 >= na), ba1 = __ballot(cum1 >= na);
             const uint64_t bb0 = __ballot(cum0 >= nb), bb1 = __ballot(cum1 >= nb);
             // first bin: lane l's bin 2l if its cum0 qualifies, else 2l + 1
@@ -629,7 +616,7 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
           wa2 = ((UA | 0x8000u) - 1u) * 0x00010001u;
           wb2 = ((UB | 0x8000u) - 1u) * 0x00010001u;
         } else {
-          kb = mean7 - FMCW_K3_KEY_LOW;
+          kb = mean7 - kK3KeyLow;
         }
         // the screen rows of the whole ring from its key16 rows (halos included)
         for (int e4 = tid; e4 < n4; e4 += NT) {
@@ -702,15 +689,8 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
           }
           cand = cfar2d_screen7_generic<NC>(rr, rlw, d0, a, need, Y);
         }
-#ifdef FMCW_K3_ABLATE  // timing experiments (tools/k3_lab): 3 = staging + cut keys only, 1 = + screen
-        if (FMCW_K3_ABLATE == 3) cand = 0u;
-        if (FMCW_K3_ABLATE == 1) cand = cand == 0xffffu ? 1u : 0u;
-#endif
       }
       uint32_t n_cand = 1u;  // candidates in the workgroup's step (nonzero: phase B runs)
-#ifdef FMCW_K3_ABLATE  // 5 = no candidate test (phase B takes every screen survivor)
-      if (FMCW_K3_ABLATE != 5)
-#endif
       {
         // (Measured and dropped: each wave testing its own survivors without workgroup barriers,
         // 643 vs 623 us per 16 frames at config 5 -- the rounds balance the waves' survivors.)
@@ -729,11 +709,6 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
             int trow, d;
             const uint32_t e = list[j];
             cell_of(e, trow, d);
-#ifdef FMCW_K3_ABLATE  // 4 = the candidate test's rounds without the test
-            if (FMCW_K3_ABLATE == 4) {
-              if (e == 0xffffffffu) atomicOr(&aux[0], 1u);
-            } else
-#endif
             if (cfar2d_exact_a<NC, HD, GD>(rr, trow, key_hi(rr.krow(trow + a.hr)[k16idx(d)]), d, a, need, sub, L) &&
                 sub == 0)
             {
@@ -745,23 +720,7 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
         cand = aux[threadIdx.x];
         n_cand = cnt[13];
         __syncthreads();  // every lane has its bits (and the count) before aux / cnt[13] change
-#ifdef FMCW_K3_COUNT  // tools/k3_lab: screen survivors and candidates into sink.counter[2], [3]
-        {
-          int s1 = __popc(scr), s2 = __popc(cand);
-          for (int o = 32; o >= 1; o >>= 1) {
-            s1 += __shfl_xor(s1, o, 64);
-            s2 += __shfl_xor(s2, o, 64);
-          }
-          if (lane == 0) {
-            atomicAdd(&sink.counter[2], (uint32_t)s1);
-            atomicAdd(&sink.counter[3], (uint32_t)s2);
-          }
-        }
-#endif
       }
-#ifdef FMCW_K3_ABLATE  // 2 = + candidate test, no phase B
-      if (FMCW_K3_ABLATE == 2) n_cand = 0u;
-#endif
       const int wtile = tile0 + f * wt_per_frame + wt0 + wv;
       // ---- Emission: the wave tile's candidates, in (range, doppler) order, go to the launch's
       // candidate list as one contiguous run (k_cfar2d_decide decides them, k_cfar2d_emit writes
@@ -859,13 +818,13 @@ __device__ __forceinline__ uint32_t cfar2d_screen_rules(const uint8_t* ab, const
   constexpr int NR = Gm::NR, RB = Gm::RB, CS = Gm::CS, NW = 2 * HR + 1;
   static_assert(Gm::N_REF == 128 && 2 * HR + 1 <= 15 && 5 * (2 * GR + 1) <= 15, "thresholds below are for n_ref 128");
   // column sums: V (seeds A/B) over the window rows, G over the guard rows, W (seeds C/D) over the box;
-  // a rolling window of K3_SCREEN_AHEAD rows of LDS reads in flight (sched_barrier + opaque sums)
+  // a rolling window of kK3ScreenAhead rows of LDS reads in flight (sched_barrier + opaque sums)
   uint32_t V[8], G[6], W[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) V[k] = W[k] = 0u;
 #pragma unroll
   for (int k = 0; k < 6; ++k) G[k] = 0u;
-  constexpr int AH = K3_SCREEN_AHEAD < NW ? K3_SCREEN_AHEAD : NW;
+  constexpr int AH = kK3ScreenAhead < NW ? kK3ScreenAhead : NW;
   int sl = rl + base;
   sl = sl >= NR ? sl - NR : sl;
   uint4 qa[AH], qb[AH], qc[AH], qd[AH];
@@ -1061,7 +1020,7 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
       __syncthreads();  // the previous step's waves are done with the rows
       if (t == t_beg) {
         // levels: the mean key7 level of the first step's CUT rows (this thread's 16 cells), then the
-        // FMCW_K3_LV_QA / _QB quantiles of a 128-bin histogram around it
+        // kK3LvQA / _QB quantiles of a 128-bin histogram around it
         float4 v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -1098,7 +1057,7 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
           int tot;
           const uint32_t ex = (uint32_t)wave_excl_scan((int)(c0 + c1), tot);
           const uint32_t cum0 = ex + c0, cum1 = ex + c0 + c1;
-          const uint32_t na = (uint32_t)(FMCW_K3_LV_QA * (TR * NC) / 1000), nb = (uint32_t)(FMCW_K3_LV_QB * (TR * NC) / 1000);
+          const uint32_t na = (uint32_t)(kK3LvQA * (TR * NC) / 1000), nb = (uint32_t)(kK3LvQB * (TR * NC) / 1000);
           const uint64_t ba0 = __ballot(cum0 >= na), ba1 = __ballot(cum1 >= na);
           const uint64_t bb0 = __ballot(cum0 >= nb), bb1 = __ballot(cum1 >= nb);
           auto first_bin = [](uint64_t m0, uint64_t m1) {
@@ -1174,13 +1133,6 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
       const bool has_tile = wv < n_wt;
       uint32_t surv = 0;
       if (has_tile && r >= HR && r < ns - HR) surv = cfar2d_screen_rules<NC, HR, GR>(ab, cd, code, base, rlw, d0, need, ruleA);
-#ifdef FMCW_K3_COUNT  // lab builds (tools/cfar2d_bench.py FMCW_K3_COUNTS=1): survivors into sink.counter[2]
-      {
-        int s1 = __popc(surv);
-        for (int o = 32; o >= 1; o >>= 1) s1 += __shfl_xor(s1, o, 64);
-        if (lane == 0) atomicAdd(&sink.counter[2], (uint32_t)s1);
-      }
-#endif
       // emission: each wave tile's survivors, in (range, doppler) order, as one run of the strip
       // buffer (flushed to the candidate list when full and at the strip's end); an empty tile is
       // final here.  (wg_base, wg_count) = (run start, run length) until k_cfar2d_emit.

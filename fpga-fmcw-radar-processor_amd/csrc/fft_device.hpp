@@ -26,16 +26,12 @@ namespace fmcw {
 // Complex arithmetic on packed fp32 (VOP3P v_pk_*_f32: one instruction per complex add, two
 // per complex product).  Left to itself the SLP vectorizer pairs components of *different*
 // complex values and then spends v_mov's re-pairing them (about a third of the FFT's VALU
-// instructions); with FMCW_PK_ASM every butterfly operation is one packed instruction on a
-// (re, im) register pair, the -i rotations and the cross terms of the product folded into
-// op_sel / neg modifiers.
-#ifndef FMCW_PK_ASM
-#define FMCW_PK_ASM 1
-#endif
+// instructions, round 2); here every butterfly operation is one packed instruction on a (re, im)
+// register pair, the -i rotations and the cross terms of the product folded into op_sel / neg
+// modifiers.
 typedef float fmcw_cf __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ fmcw_cf pk(float2 a) { return fmcw_cf{a.x, a.y}; }
 __device__ __forceinline__ float2 unpk(fmcw_cf a) { return make_float2(a.x, a.y); }
-#if FMCW_PK_ASM
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) {
   fmcw_cf r;
   asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(pk(a)), "v"(pk(b)));
@@ -46,11 +42,7 @@ __device__ __forceinline__ float2 csub(float2 a, float2 b) {
   asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(pk(a)), "v"(pk(b)));
   return unpk(r);
 }
-#ifndef FMCW_PK_CMUL_ASM
-#define FMCW_PK_CMUL_ASM 1
-#endif
 // a * b = (a.x b.x - a.y b.y, a.x b.y + a.y b.x): t = a.x * (b.x, b.y); r = t + (-a.y b.y, a.y b.x)
-#if FMCW_PK_CMUL_ASM
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   fmcw_cf t, r;
   asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(pk(a)), "v"(pk(b)));
@@ -58,11 +50,6 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
       : "=v"(r) : "v"(pk(a)), "v"(pk(b)), "v"(t));
   return unpk(r);
 }
-#else
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-#endif
 // a + (-i) d = (a.x + d.y, a.y - d.x)   and   a - (-i) d = (a.x - d.y, a.y + d.x)
 __device__ __forceinline__ float2 cadd_negi(float2 a, float2 d) {
   fmcw_cf r;
@@ -74,15 +61,6 @@ __device__ __forceinline__ float2 csub_negi(float2 a, float2 d) {
   asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(pk(a)), "v"(pk(d)));
   return unpk(r);
 }
-#else
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-__device__ __forceinline__ float2 cadd_negi(float2 a, float2 d) { return make_float2(a.x + d.y, a.y - d.x); }
-__device__ __forceinline__ float2 csub_negi(float2 a, float2 d) { return make_float2(a.x - d.y, a.y + d.x); }
-#endif
 __device__ __forceinline__ float2 mul_negi(float2 a) { return make_float2(a.y, -a.x); }  // -i a
 __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
 
@@ -101,33 +79,13 @@ __device__ __forceinline__ int opaque(int x) {
   return x;
 }
 
-// Cache policy of the streamed HBM traffic (build-time switches, measured by tools/ablate.py
-// against variant builds): NT = non-temporal (`nt` on the global load/store).
-#ifndef FMCW_NT_CUBE      // K1 loads of the input cube (read once)
-// measured on config 2 (tools/ablate.py, 20 steps): K1 0.785 -> 0.667 us/frame (6.29 TB/s),
-// K2 +0.02 us/frame; non-temporal stores of the spectrum instead cost K1 +0.03
-#define FMCW_NT_CUBE 1
-#endif
-#ifndef FMCW_NT_SPEC_ST   // K1 stores of the corner-turned spectrum (re-read by K2)
-#define FMCW_NT_SPEC_ST 0
-#endif
-#ifndef FMCW_NT_SPEC_LD   // K2 loads of the spectrum (read once)
-#define FMCW_NT_SPEC_LD 0
-#endif
-#ifndef FMCW_NT_MAP       // K2 stores of the range-Doppler map (written once)
-// measured round 2 (tools/ablate.py, variant libraries): K2 0.761 -> 0.728 us/frame with the
-// 1-D CFAR, 0.612 -> 0.528 without it; the map is never re-read by the hot path
-#define FMCW_NT_MAP 1
-#endif
-#ifndef FMCW_K1_TDIV    // K1 chirps per workgroup divided by this (>= 2 chirps kept)
-#define FMCW_K1_TDIV 1
-#endif
-#ifndef FMCW_K1_T        // K1 chirps per workgroup override (0 = by range length)
-#define FMCW_K1_T 0
-#endif
-#ifndef FMCW_K1_WAVES   // K1 waves per SIMD requested from the register allocator (0 = none)
-#define FMCW_K1_WAVES 0
-#endif
+// Cache policy of the streamed HBM traffic (measured by tools/ablate.py against variant builds,
+// DESIGN.md section 4): non-temporal (`nt`) loads of the input cube (read once; config 2, round 1:
+// K1 0.785 -> 0.667 us/frame) and non-temporal stores of the map (written once; round 2: K2 0.761
+// -> 0.728 us/frame); the corner-turned spectrum, which K2 reads back from the Infinity Cache, is
+// stored and loaded with the default policy (non-temporal spectrum loads: configs 3 / 5 -30 %,
+// round 4).
+constexpr bool kNtCube = true, kNtSpecSt = false, kNtSpecLd = false, kNtMap = true;
 typedef float fmcw_f4v __attribute__((ext_vector_type(4)));
 typedef float fmcw_f2v __attribute__((ext_vector_type(2)));
 typedef uint32_t fmcw_u2v __attribute__((ext_vector_type(2)));
@@ -174,13 +132,11 @@ template <int LR>
 __device__ __forceinline__ float2 twiddle(int e) {
   const float rev = (e > LR / 2) ? (float)(LR - e) * (1.0f / LR) : -(float)e * (1.0f / LR);
   float c = __builtin_amdgcn_cosf(rev), s = __builtin_amdgcn_sinf(rev);
-#if FMCW_PK_ASM
   // v_cos/v_sin are transcendental: a VALU reading their result needs wait states, which the
   // hazard recognizer does not insert ahead of an inline-asm reader (the packed cmul above).
   // Measured: without this, range transforms with twiddles consumed back to back came out
   // wrong (N = 4096); two wait states here make every later reader safe.
   asm volatile("s_nop 1" : "+v"(c), "+v"(s));
-#endif
   return make_float2(c, s);
 }
 

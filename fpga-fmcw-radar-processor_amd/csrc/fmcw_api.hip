@@ -48,10 +48,9 @@ __global__ void k_zero_words(uint32_t* __restrict__ a, int na, uint32_t* __restr
 // So a launch captured into a hipGraph tags its words afresh on every replay (a host-chosen epoch
 // would be baked into the graph, and a replay could take a previous replay's word for its own).
 constexpr uint32_t kLbIncl = 1u, kLbErr = 2u;
-#ifndef FMCW_DET_TILES
-#define FMCW_DET_TILES 1024
-#endif
-constexpr int kDetTiles = FMCW_DET_TILES;  // tiles (= threads) per k_det_list workgroup (256: lab A/B)
+// tiles (= threads) per k_det_list workgroup (256-tile workgroups: 10.7-10.9 / 6.0 / 8.9-9.1 us per
+// step at configs 2 / 3 / 5 against 7.4-7.6 / 5.2-5.3 / 7.2-7.3, profiles/r04/detlist/)
+constexpr int kDetTiles = 1024;
 constexpr uint32_t kLbMaxPolls = 1u << 20;  // >> any real wait (one poll ~1 us): a safety net only
 
 __device__ __forceinline__ void lb_publish(uint64_t* st, uint32_t hi, uint32_t v) {
@@ -559,14 +558,12 @@ int arm_counters(fmcw_handle* h, hipStream_t s, bool cap) {
 }
 
 constexpr size_t kCfar2Batch = 16;  // frames per 2-D CFAR launch on the caller's map (at least)
-#ifndef FMCW_K3_DECIDE_GRID
-#define FMCW_K3_DECIDE_GRID 2048
-#endif
-#ifndef FMCW_K3_EMIT_GRID
-#define FMCW_K3_EMIT_GRID 1024
-#endif
-constexpr int kCfar2DecideGrid = FMCW_K3_DECIDE_GRID;  // K3b workgroups (4 waves each, one candidate per wave at a time)
-constexpr int kCfar2EmitGrid = FMCW_K3_EMIT_GRID;      // K3c workgroups (one wave tile per wave at a time)
+// K3b / K3c grids (4 waves per workgroup; K3b one candidate per wave at a time, K3c one wave tile).
+// Round 5, with k_cfar2d_lv's ~10^5 candidates per 16-frame launch at config 5 (tools/cfar2d_bench.py,
+// profiles/r05/k3_rules/): 1024 / 256 workgroups 336 us per launch, 2048 / 256 323, 2048 / 1024
+// 302, 4096 / 2048 297; with round 4's few thousand candidates the grid was measured neutral.
+constexpr int kCfar2DecideGrid = 2048;
+constexpr int kCfar2EmitGrid = 1024;
 
 // The CFAR launcher shared by fmcw_enqueue (map just produced by K2) and fmcw_cfar.
 int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipStream_t s) {
@@ -1113,15 +1110,6 @@ int fmcw_get_info(fmcw_handle* h, int key, int64_t* value) {
     case FMCW_INFO_WINDOW_SATURATIONS: *value = h->last_status[0]; return FMCW_OK;
     case FMCW_INFO_WORD_SATURATIONS: *value = h->last_status[1]; return FMCW_OK;
     case FMCW_INFO_CFAR2D_STEPS: *value = h->cfar2_steps_last; return FMCW_OK;
-#if FMCW_LAB
-    case 100:  // FMCW_K3_COUNT builds: 2-D CFAR screen survivors / candidates since fmcw_cfar's zeroing
-    case 101: {
-      uint32_t w[4] = {0, 0, 0, 0};
-      HIP_TRY(hipMemcpy(w, h->counter, sizeof w, hipMemcpyDeviceToHost));
-      *value = w[key - 98];
-      return FMCW_OK;
-    }
-#endif
   }
   return fail(FMCW_EINVAL, "fmcw_get_info: unknown key %d", key);
 }

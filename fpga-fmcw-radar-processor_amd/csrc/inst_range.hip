@@ -56,8 +56,8 @@ RangeInfo range_info(uint32_t n, int dtype, int window, int spec, int want) {
   const bool q15 = window == FMCW_WIN_Q15_RTL;
   // the pair kernels: fp32 window, fp32 spectrum (the Q15 / fp16 / S48-spectrum paths run k_range)
   if (!q15 && spec == FMCW_SPEC_F32) {
-    if (want >= kRangePx && FMCW_K1_PX && n == 8192) return range_px(dtype);
-    if (want >= kRangeSeq && FMCW_K1_SQ && n == 4096 && n >= (uint32_t)FMCW_K1_SQ) return range_sq<4096>(dtype);
+    if (want >= kRangePx && n == 8192) return range_px(dtype);
+    if (want >= kRangeSeq && n == 4096) return range_sq<4096>(dtype);
   }
   switch (n) {
 #define R_(N) case N: return {range_fn<N>(dtype, q15, spec), RangeGeom<N>::T, RangeGeom<N>::RB, RangeGeom<N>::NT, kRangeSingle};

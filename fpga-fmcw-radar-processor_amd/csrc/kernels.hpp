@@ -23,29 +23,13 @@
 
 namespace fmcw {
 
-#ifndef FMCW_K1_HOLDW       // K1: range window held in registers: never (0), N >= 4096 (1), always (2)
-#define FMCW_K1_HOLDW 2
-#endif
-
-#ifndef FMCW_K1_WT          // K1: write-through (sc1) spectrum stores (1) or plain write-back (0)
-// measured at config 2 (two boxes): K1 62.2 -> 60.5 us per 96-frame launch, 756 -> 768 k frames/s;
-// config 3 neutral; config 5 (N = 8192) K1 64.9 -> 68.5 us per launch, so N <= 4096 only
-#define FMCW_K1_WT 1
-#endif
-#ifndef FMCW_K1_PX_POLICY   // k_range_px spectrum store cache policy bits (0 = write-back)
-#define FMCW_K1_PX_POLICY (FMCW_NT_SPEC_ST ? 2 : 0)
-#endif
-#ifndef FMCW_K2_BUFLD       // K2 prefetch through buffer loads with SGPR offsets (1) or global loads (0)
-#define FMCW_K2_BUFLD 1
-#endif
-#ifndef FMCW_K2_MAPWT       // K2: write-through (sc1) map stores (1) or non-temporal write-back (0)
-// measured at config 2: K2 55.5 -> 59.5 us per launch with write-through map stores
-#define FMCW_K2_MAPWT 0
-#endif
-
-#ifndef FMCW_CFAR1D_WHOLE   // 1-D screen over the lane's whole window (1) or two 8-cell halves (0)
-#define FMCW_CFAR1D_WHOLE 1
-#endif
+// K1 spectrum stores at N <= 4096 are write-through (sc1): measured at config 2 (two boxes) K1
+// 62.2 -> 60.5 us per 96-frame launch, 756 -> 768 k frames/s; config 3 neutral; config 5 (N = 8192)
+// K1 64.9 -> 68.5 us per launch with them, so k_range_px stores write-back.  K2's map stores stay
+// non-temporal write-back (write-through: K2 55.5 -> 59.5 us per launch at config 2).  Every other
+// alternative measured in rounds 1-4 ("removed after measurement") is gone
+// from the sources; the numbers stay in DESIGN.md and the lab builds in git history.
+constexpr bool kK1WriteThrough = true;
 
 // --------------------------------------------------------------------------------------
 // Input loaders: two consecutive complex samples -> float4 (re0, im0, re1, im1).
@@ -65,12 +49,12 @@ struct LoadF32 {
   using Raw = float4;
   using Raw1 = float2;
   __device__ __forceinline__ static Raw fetch(const void* base, size_t idx) {
-    return ld_f4<FMCW_NT_CUBE>(reinterpret_cast<const float2*>(base) + idx);
+    return ld_f4<kNtCube>(reinterpret_cast<const float2*>(base) + idx);
   }
   __device__ __forceinline__ static float4 expand(Raw r) { return r; }
   __device__ __forceinline__ static float4 load2(const void* base, size_t idx) { return fetch(base, idx); }
   __device__ __forceinline__ static Raw1 fetch1(const void* base, size_t idx) {
-    return ld_f2<FMCW_NT_CUBE>(reinterpret_cast<const float2*>(base) + idx);
+    return ld_f2<kNtCube>(reinterpret_cast<const float2*>(base) + idx);
   }
   __device__ __forceinline__ static float2 expand1(Raw1 r) { return r; }
   __device__ __forceinline__ static float2 expand1_scaled(Raw1 r, float s) { return make_float2(r.x * s, r.y * s); }
@@ -80,7 +64,7 @@ struct LoadF16 {
   using Raw = fmcw_u2v;
   using Raw1 = uint32_t;
   __device__ __forceinline__ static Raw fetch(const void* base, size_t idx) {
-    return ld_u2<FMCW_NT_CUBE>(reinterpret_cast<const uint32_t*>(base) + idx);
+    return ld_u2<kNtCube>(reinterpret_cast<const uint32_t*>(base) + idx);
   }
   __device__ __forceinline__ static float4 expand(Raw u) {
     typedef _Float16 h4 __attribute__((ext_vector_type(4)));
@@ -89,7 +73,7 @@ struct LoadF16 {
   }
   __device__ __forceinline__ static float4 load2(const void* base, size_t idx) { return expand(fetch(base, idx)); }
   __device__ __forceinline__ static Raw1 fetch1(const void* base, size_t idx) {
-    return ld_u1<FMCW_NT_CUBE>(reinterpret_cast<const uint32_t*>(base) + idx);
+    return ld_u1<kNtCube>(reinterpret_cast<const uint32_t*>(base) + idx);
   }
   __device__ __forceinline__ static float2 expand1(Raw1 u) {
     typedef _Float16 h2 __attribute__((ext_vector_type(2)));
@@ -110,7 +94,7 @@ struct LoadI16 {
   using Raw = fmcw_u2v;
   using Raw1 = uint32_t;
   __device__ __forceinline__ static Raw fetch(const void* base, size_t idx) {
-    return ld_u2<FMCW_NT_CUBE>(reinterpret_cast<const uint32_t*>(base) + idx);
+    return ld_u2<kNtCube>(reinterpret_cast<const uint32_t*>(base) + idx);
   }
   __device__ __forceinline__ static float4 expand(Raw u) {
     typedef short s4 __attribute__((ext_vector_type(4)));
@@ -119,7 +103,7 @@ struct LoadI16 {
   }
   __device__ __forceinline__ static float4 load2(const void* base, size_t idx) { return expand(fetch(base, idx)); }
   __device__ __forceinline__ static Raw1 fetch1(const void* base, size_t idx) {
-    return ld_u1<FMCW_NT_CUBE>(reinterpret_cast<const uint32_t*>(base) + idx);
+    return ld_u1<kNtCube>(reinterpret_cast<const uint32_t*>(base) + idx);
   }
   __device__ __forceinline__ static float2 expand1(Raw1 u) {
     typedef short s2 __attribute__((ext_vector_type(2)));
@@ -233,8 +217,7 @@ template <int N> struct RangeGeom {
   // (4 waves, 35 KiB LDS, 3 workgroups per CU at 141 VGPRs) beats T = 8 (8 waves, one
   // workgroup per CU) by 9 % in K1 with K2 unchanged; T = 2 is 3 % faster again in K1 but
   // halves K2's read runs (64 B) and costs more there than it saves.
-  static constexpr int T0 = FMCW_K1_T > 0 && N == 1024 ? FMCW_K1_T : N <= 128 ? 16 : N <= 512 ? 8 : N == 1024 ? 4 : 2;
-  static constexpr int T = T0 / FMCW_K1_TDIV >= 2 ? T0 / FMCW_K1_TDIV : 2;
+  static constexpr int T = N <= 128 ? 16 : N <= 512 ? 8 : N == 1024 ? 4 : 2;
   static constexpr int NT = T * P;                   // threads per workgroup
   static constexpr int RB = 128 / T;                 // range bins per 1 KiB chunk
   static constexpr int REG = padded(N) + 4;          // LDS row (complex) per chirp
@@ -253,7 +236,7 @@ template <int N> struct RangeGeom {
 // SP_S48 (FMCW_SPEC_S48, T >= 4) two 6-B S48 points (12-B stores).
 template <int N, typename LD, bool Q15 = false, int SP = SP_F32>
 __global__ void __launch_bounds__(RangeGeom<N>::NT)
-__attribute__((amdgpu_waves_per_eu(FMCW_K1_WAVES > 0 && N < 8192 ? FMCW_K1_WAVES : 1)))
+__attribute__((amdgpu_waves_per_eu(1)))
 k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* __restrict__ win,
         const float* __restrict__ chirp_w, int nc, int n_groups, float q15_scale, uint32_t* __restrict__ status) {
   using Gm = RangeGeom<N>;
@@ -291,11 +274,9 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
     for (int m = 0; m < 8; ++m) a[m] = LD::fetch(cube, chirp * N + 2 * t0 + (N / 8) * m);
     if (chirp_w) cw_n = chirp_w[cw_index(cb * T + q)];
   }
-  // window coefficients for samples 2t + {0,1} + (N/8) m.  N >= 4096 (one or two workgroups
-  // per CU, so nothing else hides that store wait): held for the whole kernel.  Smaller N:
-  // re-read (L1/L2 hits) every group, 16 VGPRs fewer across the LDS passes (the register peak
-  // at 3 workgroups per CU).
-  constexpr bool HOLD_W = FMCW_K1_HOLDW >= 2 || (FMCW_K1_HOLDW == 1 && N >= 4096);
+  // window coefficients for samples 2t + {0,1} + (N/8) m, held for the whole kernel (round 4:
+  // re-reading them every group below N = 4096 measured 845-848 k against 856-857 k frames/s)
+  constexpr bool HOLD_W = true;
   float2 wh[HOLD_W ? 8 : 1];
   if constexpr (HOLD_W) {
 #pragma unroll
@@ -372,7 +353,7 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
     float2* dst = inter + dbase;
     uint2* dst16 = reinterpret_cast<uint2*>(reinterpret_cast<uint32_t*>(inter) + dbase);
     const size_t dstep = (size_t)CI * ncb * (RB * T);
-    // FMCW_K1_WT: write-through stores (the launch's spectrum is < 4 GiB: fmcw_create caps the chunk)
+    // write-through stores (the launch's spectrum is < 4 GiB: fmcw_create caps the chunk)
     const __amdgpu_buffer_rsrc_t wrs = wt_rsrc(inter, 0xffffffffu);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -389,10 +370,10 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
         static_assert(T >= 4, "S48 shares an exponent over 4 chirps of a tile row");
         __builtin_amdgcn_raw_buffer_store_b96(s48_pack_pair(v0, v1, c0 & 3), wrs,
                                               (uint32_t)((dbase + i * dstep) * sizeof(S48)), 0,
-                                              FMCW_K1_WT ? 16 /* sc1 */ : 0);
+                                              kK1WriteThrough ? 16 /* sc1 */ : 0);
       }
-      else if constexpr (FMCW_K1_WT && N <= 4096) st_f4_wt(wrs, (uint32_t)((dbase + i * dstep) * sizeof(float2)), make_float4(v0.x, v0.y, v1.x, v1.y));
-      else st_f4<FMCW_NT_SPEC_ST>(dst + i * dstep, make_float4(v0.x, v0.y, v1.x, v1.y));
+      else if constexpr (kK1WriteThrough && N <= 4096) st_f4_wt(wrs, (uint32_t)((dbase + i * dstep) * sizeof(float2)), make_float4(v0.x, v0.y, v1.x, v1.y));
+      else st_f4<kNtSpecSt>(dst + i * dstep, make_float4(v0.x, v0.y, v1.x, v1.y));
     }
   }
   if constexpr (Q15) status_add(status, n_sat);  // status word 2 (status = n_dets_dev + 2): window saturations
@@ -418,9 +399,6 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
 // registers (one chirp ahead, whatever group it belongs to), so the load overlaps three LDS passes.
 // Replaces the Xilinx range FFT (rtl/src/radar_core.vhd:303-316) + corner turner (:318-327).
 // --------------------------------------------------------------------------------------
-#ifndef FMCW_K1_SQ         // smallest N that runs k_range_sq (0: never; N = 8192 runs k_range_px)
-#define FMCW_K1_SQ 4096
-#endif
 template <int N, int V> struct SqGeom {
   static constexpr int P = N / V;
   static constexpr int T = 2, RB = 64;          // = RangeGeom<N> for N >= 2048
@@ -520,7 +498,7 @@ k_range_sq(const void* __restrict__ cube, float2* __restrict__ inter, const floa
     // profiles/r04/k1/policy/; nt + sc1 7 % slower)
     const int t = opaque(t0);
     const size_t fbase = (size_t)fr * N * nc;
-    constexpr bool WT = FMCW_K1_WT && N <= 4096;
+    constexpr bool WT = kK1WriteThrough && N <= 4096;
     const __amdgpu_buffer_rsrc_t srs = wt_rsrc(inter + fbase, 0xffffffffu);  // one frame's tiles < 4 GiB
 #pragma unroll
     for (int gg = 0; gg < GF; ++gg)
@@ -530,7 +508,7 @@ k_range_sq(const void* __restrict__ cube, float2* __restrict__ inter, const floa
         const size_t off = ((size_t)(d / RB) * ncb + cb) * (RB * T) + (size_t)(d % RB) * T;
         const float4 x = make_float4(X[0][gg][m].x, X[0][gg][m].y, X[1][gg][m].x, X[1][gg][m].y);
         if constexpr (WT) st_f4_wt(srs, (uint32_t)(off * sizeof(float2)), x);
-        else st_f4<FMCW_NT_SPEC_ST>(inter + fbase + off, x);
+        else st_f4<kNtSpecSt>(inter + fbase + off, x);
       }
   }
 }
@@ -556,9 +534,6 @@ k_range_sq(const void* __restrict__ cube, float2* __restrict__ inter, const floa
 // as 16-B (chirp 0, chirp 1) tile elements: lanes 0-31 and 32-63 each write 512 contiguous bytes.
 // Replaces the Xilinx range FFT (rtl/src/radar_core.vhd:303-316) + corner turner (:318-327).
 // --------------------------------------------------------------------------------------
-#ifndef FMCW_K1_PX          // k_range_px at N = 8192 (1) or k_range_sq (0)
-#define FMCW_K1_PX 1
-#endif
 __device__ __forceinline__ void swap32(float2& a, float2& b) {
   // a, b := [a_lo, b_lo], [a_hi, b_hi] (lo / hi = lanes 0-31 / 32-63)
   const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.x), __float_as_uint(b.x), false, false);
@@ -591,7 +566,7 @@ k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const floa
   // SGPR offset (no 64-bit address per load / store in VGPRs)
   using Raw1 = typename LD::Raw1;
   constexpr int SB = sizeof(Raw1);  // bytes per sample
-  constexpr int NTL = FMCW_NT_CUBE ? 2 : 0;  // non-temporal cube loads (read once)
+  constexpr int NTL = kNtCube ? 2 : 0;  // non-temporal cube loads (read once)
   Raw1 a[16];
   float cwn = 1.f;
   auto fetch = [&](int g, int q) {
@@ -603,12 +578,6 @@ k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const floa
     const int vo = opaque(t0) * SB;
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
-#if defined(FMCW_K1_ABLATE) && FMCW_K1_ABLATE == 2  // timing experiments (tools/k1_lab): no cube loads
-      if constexpr (SB == 4) {
-        a[m] = __builtin_bit_cast(Raw1, (uint32_t)(vo * 0x9e3779b1u + m + (uint32_t)chirp));
-        continue;
-      }
-#endif
       if constexpr (SB == 4) {
         a[m] = __builtin_bit_cast(Raw1, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, m * 512 * SB, NTL));
       } else {
@@ -655,9 +624,6 @@ k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const floa
       // the next chirp's input: this group's second chirp, or the next group's first
       if (q == 0) fetch(g, 1);
       else if (g + (int)gridDim.x < n_groups) fetch(g + gridDim.x, 0);
-#if defined(FMCW_K1_ABLATE) && FMCW_K1_ABLATE == 3  // timing experiments: no pass B (wrong results)
-      if (false)
-#endif
       {  // pass B: radix 16, L = 16 (in place, barriers around the exchange)
         __syncthreads();
         float2 v[16];
@@ -718,11 +684,8 @@ k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const floa
         const int r = s ? m : m + 8;
         typedef float f4v __attribute__((ext_vector_type(4)));
         const f4v x = {X[0][r].x, X[0][r].y, X[1][r].x, X[1][r].y};
-#if defined(FMCW_K1_ABLATE) && FMCW_K1_ABLATE == 1  // timing experiments: no spectrum stores
-        if (x.x != 1234.5f) continue;
-#endif
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(fmcw_u4v, x), rs, vo, (4 * m + 64 * s) * ncb * 1024,
-                                               FMCW_K1_PX_POLICY);
+                                               0 /* write-back */);
       }
   }
 }
@@ -914,15 +877,12 @@ __device__ __forceinline__ void load_cells(const float* base, int o0, float (&v)
 // --------------------------------------------------------------------------------------
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
-#ifndef FMCW_K2_WPB_1024  // K2 / 1-D CFAR waves per workgroup at NC = 1024 (4 or 8)
-#define FMCW_K2_WPB_1024 4
-#endif
 template <int NC> struct DopplerGeom {
   static constexpr int P = NC / 16;                     // lanes per range row (16 cells each)
   static constexpr int WR = 64 / P;                     // range rows per wave tile
   // waves per workgroup (independent; a workgroup's waves take consecutive row groups of one
   // frame, so together they read WPB x WR x T x 8 B of every 1 KiB spectrum tile)
-  static constexpr int WPB = NC >= 1024 ? FMCW_K2_WPB_1024 : 4;
+  static constexpr int WPB = 4;  // (8 at NC = 1024, one workgroup reading whole 128-B lines: 56.5 -> 65.3 us)
   static constexpr int NT = 64 * WPB;
   static constexpr int REGD = padded(NC) + 4;           // complex per range row (FFT)
   static constexpr int REGM = mrow_floats<NC>();        // floats per magnitude row
@@ -1046,7 +1006,6 @@ __device__ __forceinline__ void cfar1d_wave(const float* mags, uint32_t* list, i
     const float* lb = mrow + midx(d0);
     const int need = nref - cf.rank;
     constexpr bool one_group = ONEG;           // the reference (rank 12 of 16): any group rejects
-#if FMCW_CFAR1D_WHOLE
     // The lane's whole window at once: cells d0 - H .. d0 + 15 + H, group minima g[k] =
     // min(w[k .. k+3]) over it computed once (2 mins per group), not per 8-cell half.
     {
@@ -1095,59 +1054,10 @@ __device__ __forceinline__ void cfar1d_wave(const float* mags, uint32_t* list, i
         bits |= sb << i;
       }
     }
-#else
-    constexpr int HC = CELLS / 2, WH = HC + 2 * H;
-    constexpr int NV = (WH + 3 + 3) / 4;       // 16-B reads covering the window from floor4
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      const int ws = hh * HC - H;              // first window cell relative to d0
-      const int o0 = floor4(ws);
-      float v[4 * NV];
-      load_cells<NV>(lb, o0, v);
-      float w[WH];
-#pragma unroll
-      for (int k = 0; k < WH; ++k) w[k] = v[ws - o0 + k];
-      float g[WH - 3];                         // g[k] = min(w[k .. k+3])
-      {
-        float m2[WH - 1];
-#pragma unroll
-        for (int k = 0; k < WH - 1; ++k) m2[k] = fminf(w[k], w[k + 1]);
-#pragma unroll
-        for (int k = 0; k < WH - 3; ++k) g[k] = fminf(m2[k], m2[k + 2]);
-      }
-#pragma unroll
-      // survivor bits by integer arithmetic on the (non-negative) float patterns: a float
-      // compare would produce one SGPR-pair lane mask per cell and push the kernel into SGPR
-      // spills (v_readlane/v_writelane in the tile loop)
-      for (int i = 0; i < HC; ++i) {
-        const uint32_t cbits = __float_as_uint(w[H + i]);
-        uint32_t sb;
-        if (one_group) {
-          float M = g[i];
-#pragma unroll
-          for (int q = 1; q < NGS; ++q) M = fmaxf(M, g[i + 4 * q]);
-#pragma unroll
-          for (int q = 0; q < NGS; ++q) M = fmaxf(M, g[i + RO + 4 * q]);
-          sb = lt_bit(__float_as_uint(cf.alpha * M), cbits);  // alpha M < cut
-        } else {
-          uint32_t nlt = 0;  // groups with alpha * min < cut
-#pragma unroll
-          for (int q = 0; q < NGS; ++q)
-            nlt += lt_bit(__float_as_uint(cf.alpha * g[i + 4 * q]), cbits) +
-                   lt_bit(__float_as_uint(cf.alpha * g[i + RO + 4 * q]), cbits);
-          sb = 4 * (2 * NGS - (int)nlt) < need ? 1u : 0u;
-        }
-        bits |= sb << (hh * HC + i);
-      }
-    }
-#endif
     // Exact count for the survivors only, one survivor per lane.  About 12 of a tile's 1024
     // cells survive the screen on noise + targets, but they sit in ~8 of the 16 cell
     // indices, so counting per index for the whole wave (where any lane survived) cost 8 x 16
     // compares per lane; the ordered survivor list costs one 16-compare round per 64.
-#ifdef FMCW_CFAR1D_ABLATE  // timing experiments only: 2 = screen, no exact round
-    if (FMCW_CFAR1D_ABLATE == 2) bits = 0;
-#endif
     int n_surv;
     const int sx = wave_excl_scan(__popc(bits), n_surv);
     if (n_surv != 0) {  // uniform
@@ -1399,15 +1309,6 @@ __device__ __forceinline__ float2 win_q15c(float2 x, float c, uint32_t& n) {
   return make_float2((float)si, (float)sq);
 }
 
-#ifndef FMCW_K2_SOFF_CHAIN  // K2 prefetch: the SGPR load offsets advanced per load, not hoisted (1)
-#define FMCW_K2_SOFF_CHAIN 1
-#endif
-#ifndef FMCW_K2_PREFETCH  // K2 (MTI off): points of the next (tile, rx) unit loaded ahead (0, 8 or 16)
-#define FMCW_K2_PREFETCH 16
-#endif
-#ifndef FMCW_K2_XCD       // K2: contiguous logical workgroup ids per XCD (1)
-#define FMCW_K2_XCD 1
-#endif
 // Workgroups are dispatched round-robin over the 8 XCDs (XCD = id % 8, MI355X_MICROARCH.md).
 // Giving each XCD a contiguous range of logical ids puts neighbouring tiles -- which read the
 // two halves of the same 128-B lines of the tiled spectrum when a workgroup covers only 64 B of
@@ -1417,51 +1318,27 @@ __device__ __forceinline__ int xcd_block_id(int bid, int grid) {
   return (bid & 7) * (grid >> 3) + (bid >> 3);
 }
 
-#ifndef FMCW_K2_ORDER     // K2 tile order (see k_doppler)
-#define FMCW_K2_ORDER 1
-#endif
-#ifndef FMCW_K2_PF_NC     // K2: largest NC with the next-unit register prefetch
-#define FMCW_K2_PF_NC 256  // measured: no gain at NC = 512, 1024 (profiles/r02/k2_pf); again after
-                           // the one-site prefetch: NC 512 41.0 vs 41.2 us, NC 1024 62.8 vs 55.4 us
-#endif
-#ifndef FMCW_K2_PREFETCH_1024  // K2 at NC = 1024 (MTI off): none (8 or 16 points: slower, below)
-#define FMCW_K2_PREFETCH_1024 0
-#endif
-#ifndef FMCW_K2_PREFETCH_512  // K2 at NC = 512 (MTI off): points of the next unit loaded ahead
-#define FMCW_K2_PREFETCH_512 8  // half a unit: 165 instead of 178 VGPRs, so 3 waves per SIMD
-                                // instead of 2, and config-3 K2 41.6-41.9 -> 39.0-39.2 us per
-                                // launch (profiles/r03/k2/k2_pf_ab.log; 16 points: 42.1, 3 waves
-                                // without a prefetch: 42.2-42.5; at NC = 1024 both slower, 61-64
-                                // against 56 us)
-#endif
-#ifndef FMCW_K2_WAVES     // K2 waves per SIMD asked of the register allocator (0 = by geometry)
-#define FMCW_K2_WAVES 0
-#endif
+// K2's register prefetch of the next (tile, rx) unit (MTI off), points loaded ahead: all 16 up to
+// NC = 256; 8 (half a unit) at NC = 512, which fits 165 instead of 178 VGPRs and so 3 waves per
+// SIMD (config-3 K2 41.6-41.9 -> 39.0-39.2 us per launch, profiles/r03/k2/k2_pf_ab.log; 16 points
+// 42.1, none 42.2-42.5); none at NC = 1024 (8 or 16 points: 61-64 against 56 us).
+template <int NC, int MTI>
+constexpr int k2_prefetch() { return MTI != 0 ? 0 : NC <= 256 ? 16 : NC == 512 ? 8 : 0; }
 // FAST (below) at NC = 256 fits 128 VGPRs without scratch: 4 waves per SIMD (4 workgroups of
 // 39 KiB LDS per CU); measured K2 58.2 -> 56.0 us per 96-frame launch at config 2.  At NC = 512
 // / 1024 the fourth wave costs more than it hides (config 3 K2 41.7 -> 55.9 us, config 5 55.5
-// -> 74.6 us per launch; gpurun_out bench_libs, round 2).
-#ifndef FMCW_K2_S48_WAVES  // lab A/B: waves per SIMD of the S48 K2 (0 = as fp32)
-#define FMCW_K2_S48_WAVES 0
-#endif
-#ifndef FMCW_K2_S48_PF     // lab A/B: points prefetched by the S48 K2 at NC <= FMCW_K2_PF_NC
-#define FMCW_K2_S48_PF 16
-#endif
-template <int NC, int MTI, bool FAST = false, int SP = SP_F32>
-constexpr int k2_waves() {
-  return FMCW_K2_WAVES > 0                 ? FMCW_K2_WAVES
-         : (SP == SP_S48 && FMCW_K2_S48_WAVES > 0) ? FMCW_K2_S48_WAVES
-         : (FAST && MTI == 0 && NC == 256) ? 4
-         : (MTI == 0 && NC <= 256 && FMCW_K2_PREFETCH <= 8) ? 3
-                                                            : 2;
-}
+// -> 74.6 us per launch; gpurun_out bench_libs, round 2).  The S48 FAST K2 at NC = 256: 4 waves
+// (128 VGPRs, 16 B of scratch) measured 0.570 us per frame, 3 waves 0.584-0.598, an 8-point
+// prefetch 0.571-0.574 (profiles/r05/spec_ab/).
+template <int NC, int MTI, bool FAST = false>
+constexpr int k2_waves() { return (FAST && MTI == 0 && NC == 256) ? 4 : 2; }
 // FAST: the common configuration fixed at compile time -- |X| magnitude (no AMBM), no dB map,
 // and the 1-D CFAR, when enabled, at the reference geometry (8 refs / 2 guards per side, need =
 // n_ref - rank <= 4, fp32 compare).  The generic kernel keeps those as uniform runtime branches,
 // whose other arms held registers and SGPRs (spills to VGPR lanes) across the tile loop.
 // SP: the spectrum format K1 wrote (SP_F32, SP_F16, SP_S48; S48 with MTI off, P % 4 == 0 and T >= 4).
 template <int NC, int MTI, int SP = SP_F32, bool FAST = false>
-__global__ void __launch_bounds__(DopplerGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(k2_waves<NC, MTI, FAST, SP>())))
+__global__ void __launch_bounds__(DopplerGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(k2_waves<NC, MTI, FAST>())))
 k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, int ns, int nrx,
           int lgT, int lgRB, int n_tiles, int frame0, int tile0, float* __restrict__ lin_map,
           float* __restrict__ db_map, int mag_mode, int mti_rtl, int q15d, Cfar1DArgs cf, DetSink sink,
@@ -1515,18 +1392,14 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
   // registers right after this unit's first pass has consumed its own, so a wave keeps 8 KiB
   // of HBM reads in flight through its FFT, magnitude, map store and CFAR phases instead of
   // exposing the full load latency once per unit.
-  constexpr int NPF = MTI != 0                ? 0
-                      : NC <= FMCW_K2_PF_NC     ? (SP == SP_S48 ? FMCW_K2_S48_PF : FMCW_K2_PREFETCH)
-                      : NC == 512               ? FMCW_K2_PREFETCH_512
-                      : NC == 1024              ? FMCW_K2_PREFETCH_1024
-                                                : 0;  // points loaded ahead
+  constexpr int NPF = k2_prefetch<NC, MTI>();  // points loaded ahead
   constexpr bool PF = NPF > 0;
-  // Tile order.  FMCW_K2_ORDER 0: frame-minor over all waves (tile -> f = tile % nf).
-  // Measured on config 2: order 1 cuts K2 0.905 -> 0.874 us/frame (map-store cost 0.13 -> 0.085).
-  // FMCW_K2_ORDER 1: the WPB waves of a workgroup take WPB consecutive wave tiles (row
-  // groups) of one frame, frame-minor over workgroups, so the 4 x WR rows they read from
-  // each 1 KiB block of the tiled spectrum are requested together (DRAM page locality).
-  const bool grp = FMCW_K2_ORDER != 0 && tiles_per_frame % WPB == 0;
+  // Tile order: the WPB waves of a workgroup take WPB consecutive wave tiles (row groups) of one
+  // frame, frame-minor over workgroups, so the 4 x WR rows they read from each 1 KiB block of the
+  // tiled spectrum are requested together (DRAM page locality; round 1, config 2: K2 0.905 ->
+  // 0.874 us/frame against frame-minor over all waves, which remains for frames whose tile count
+  // is not a multiple of WPB).
+  const bool grp = tiles_per_frame % WPB == 0;
   auto tile_fl = [&](int tl, int& fo, int& lo) {
     if (grp) {
       const int u = tl / WPB;
@@ -1546,7 +1419,7 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
            off_of((uint32_t)(ru >> lgRB) << lgncb, (uint32_t)(ru & ((1 << lgRB) - 1)), 0);
   };
   float2 nxt[PF ? NPF : 1];
-  const __amdgpu_buffer_rsrc_t srs = wt_rsrc(const_cast<SE*>(inter), 0xffffffffu);  // FMCW_K2_BUFLD
+  const __amdgpu_buffer_rsrc_t srs = wt_rsrc(const_cast<SE*>(inter), 0xffffffffu);  // the prefetch's buffer loads
   // last-pass twiddle bases, once per lane (NC = 256: pass 1 + one radix-16 pass, k = t)
   constexpr bool TWH = NC / 16 <= 16 && P % 16 == 0;
   GroupTwiddles<NC / 16, NC> twh;
@@ -1571,22 +1444,22 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
               const uint32_t vo = (uint32_t)((const char*)pb - (const char*)inter) - (s48_sh(tq) >> 3);
               typedef float f2v __attribute__((ext_vector_type(2)));
               const f2v r = __builtin_bit_cast(
-                  f2v, __builtin_amdgcn_raw_buffer_load_b64(srs, vo, so, FMCW_NT_SPEC_LD ? 2 /* nt */ : 0));
+                  f2v, __builtin_amdgcn_raw_buffer_load_b64(srs, vo, so, kNtSpecLd ? 2 /* nt */ : 0));
               nxt[m] = make_float2(r.x, r.y);
               so += sb;
-              if constexpr (FMCW_K2_SOFF_CHAIN) asm volatile("" : "+s"(so));
-            } else if constexpr (SP == SP_F32 && FMCW_K2_BUFLD) {
+              asm volatile("" : "+s"(so));
+            } else if constexpr (SP == SP_F32) {
               // buffer load: lane offset in a VGPR, the uniform m S in an SGPR (no 64-bit VALU
               // address add per load; the chunk's spectrum is < 4 GiB, fmcw_create caps it)
               const uint32_t vo = (uint32_t)((const char*)pb - (const char*)inter);
               typedef float f2v __attribute__((ext_vector_type(2)));
               const f2v r = __builtin_bit_cast(
-                  f2v, __builtin_amdgcn_raw_buffer_load_b64(srs, vo, so, FMCW_NT_SPEC_LD ? 2 /* nt */ : 0));
+                  f2v, __builtin_amdgcn_raw_buffer_load_b64(srs, vo, so, kNtSpecLd ? 2 /* nt */ : 0));
               nxt[m] = make_float2(r.x, r.y);
               so += sb;
-              if constexpr (FMCW_K2_SOFF_CHAIN) asm volatile("" : "+s"(so));
+              asm volatile("" : "+s"(so));
             } else {
-              nxt[m] = ld_spec<FMCW_NT_SPEC_LD>(pb + (size_t)m * S, sscale);
+              nxt[m] = ld_spec<kNtSpecLd>(pb + (size_t)m * S, sscale);
             }
           }
         } else {
@@ -1595,10 +1468,10 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
             const uint32_t c = (uint32_t)(tq + P * m);
             const SE* pc = p + ((((c >> lgT) << lgRB) << lgT) | (c & (uint32_t)(T - 1)));
             if constexpr (SP == SP_S48) {
-              const fmcw_u2v r = ld_s48_raw<FMCW_NT_SPEC_LD>(pc, (uint32_t)tq & 1u);
+              const fmcw_u2v r = ld_s48_raw<kNtSpecLd>(pc, (uint32_t)tq & 1u);
               nxt[m] = make_float2(__uint_as_float(r.x), __uint_as_float(r.y));
             } else {
-              nxt[m] = ld_spec<FMCW_NT_SPEC_LD>(pc, sscale);
+              nxt[m] = ld_spec<kNtSpecLd>(pc, sscale);
             }
           }
         }
@@ -1608,7 +1481,7 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
   // XCD-contiguous ids only where a workgroup reads less than a 128-B line of each tile
   // (measured: config 5 K2 177 -> 110 us per 4 frames; configs 2 / 3, whose workgroups read
   // whole lines, 2-3 % slower with it)
-  const bool xcd = FMCW_K2_XCD && ((WPB * WR * 8) << lgT) < 128;
+  const bool xcd = ((WPB * WR * 8) << lgT) < 128;
   const int bid = xcd ? xcd_block_id((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
   prefetch(bid * WPB + wv, 0);
 
@@ -1632,8 +1505,8 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
     for (int rx = 0; rx < nrx; ++rx) {
       const SE* src = inter + ((size_t)f * nrx + rx) * (size_t)ns * NC;
       auto at = [&](uint32_t c) -> float2 {
-        if constexpr (SP == SP_S48) return s48_unpack(ld_s48_raw<FMCW_NT_SPEC_LD>(src + off_of(rbase, rin, c), c & 1u), (uint32_t)t & 1u, s48_q2(t));
-        else return ld_spec<FMCW_NT_SPEC_LD>(src + off_of(rbase, rin, c), sscale);
+        if constexpr (SP == SP_S48) return s48_unpack(ld_s48_raw<kNtSpecLd>(src + off_of(rbase, rin, c), c & 1u), (uint32_t)t & 1u, s48_q2(t));
+        else return ld_spec<kNtSpecLd>(src + off_of(rbase, rin, c), sscale);
       };
       float2 v[16];
 #pragma unroll
@@ -1668,9 +1541,7 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
         }
         v[m] = x;
       }
-#ifndef FMCW_K2_ABLATE_FFT  // timing experiments only (round 4): 1 = no FFT arithmetic (data movement kept)
       Dft<16>::run(v);                       // pass 1: L = 1, no twiddles
-#endif
       {
         float2* d = buf + pad16(16 * t);     // y[16 t + m]
 #pragma unroll
@@ -1683,12 +1554,6 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
         prefetch(same ? tile : tile + tile_step, same ? rx + 1 : 0);
       }
       float2 X[LG][LR];
-#ifdef FMCW_K2_ABLATE_FFT
-      if constexpr (TWH) {
-#pragma unroll
-        for (int m = 0; m < 16; ++m) X[0][m] = buf[pad16(t) + padoff(m * 16)];
-      } else
-#endif
       if constexpr (TWH) stockham_last_tw<NC, 16, P>(buf, t, X, twh);
       else stockham_to_regs<NC, 16, P, false>(buf, t, X);
       if (!FAST && mag_mode == FMCW_MAG_AMBM) {  // uniform: one branch for the whole block
@@ -1726,7 +1591,6 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
 
     // map store: WR*NC = 1024 floats contiguous at [f][r0][0], 16 B per lane
     {
-      const __amdgpu_buffer_rsrc_t mrs = wt_rsrc(lin_map, 0xffffffffu);  // a launch's map < 4 GiB
       constexpr int Q = WR * NC / 4 / 64;
       const size_t mbase = ((size_t)f * ns + r0) * NC;
       const int lane = opaque(lane0);
@@ -1736,8 +1600,7 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
         const int rl = e / NC, d = e - rl * NC;
         const float4 v = *reinterpret_cast<const float4*>(mags + rl * REGM + midx(d));
         if (lin_map) {
-          if constexpr (FMCW_K2_MAPWT) st_f4_wt(mrs, (uint32_t)((mbase + e) * sizeof(float)), v);
-          else st_f4<FMCW_NT_MAP>(lin_map + mbase + e, v);
+          st_f4<kNtMap>(lin_map + mbase + e, v);
         }
         if (!FAST && db_map) {
           const float k = 6.0205999132796239f;  // 20 / log2(10)
@@ -1747,11 +1610,7 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
         }
       }
     }
-    if (cf.enabled)
-#ifdef FMCW_CFAR1D_ABLATE  // 1 = halos only, no CFAR
-      if (FMCW_CFAR1D_ABLATE != 1)
-#endif
-    {
+    if (cf.enabled) {
       if constexpr (FAST)
         cfar1d_wave<NC, 8, 2, true>(mags, list, rr, t, r0, frame0 + f, tile0 + f * tiles_per_frame + lt, cf, sink);
       else

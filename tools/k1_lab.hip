@@ -1,3 +1,7 @@
+// NOTE (round 5): the kernel sources no longer carry build-time switches or ablation blocks
+// (csrc/*.hpp, DESIGN.md section 4 "Build-time constants").  This lab program still builds and
+// times the shipped kernels; its -D variants (FMCW_K3_ABLATE, FMCW_K1_ABLATE, FMCW_K3_KEY_*, ...)
+// refer to the sources at commit 72a93dd, where the measurements in profiles/r03-r04 were taken.
 // k1_lab.hip -- stand-alone timing / agreement harness for the range-stage (K1) variants.
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -o tools/k1_lab tools/k1_lab.hip
 // Run:   tools/k1_lab <N> <n_chirps> <n_rx> <frames> <f16:0|1> [reps]

@@ -1,3 +1,7 @@
+// NOTE (round 5): the kernel sources no longer carry build-time switches or ablation blocks
+// (csrc/*.hpp, DESIGN.md section 4 "Build-time constants").  This lab program still builds and
+// times the shipped kernels; its -D variants (FMCW_K3_ABLATE, FMCW_K1_ABLATE, FMCW_K3_KEY_*, ...)
+// refer to the sources at commit 72a93dd, where the measurements in profiles/r03-r04 were taken.
 // k3_lab.hip -- stand-alone timing / exactness harness for the 2-D OS-CFAR (K3) variants at
 // BASELINE config 5's map geometry (8192 range x 1024 Doppler, 2-D CFAR with the reference
 // window of rtl/src/os_cfar_2d.vhd as instantiated at radar_core.vhd:376-382).
