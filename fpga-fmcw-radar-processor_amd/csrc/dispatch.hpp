@@ -20,8 +20,8 @@ struct RangeInfo {
   int kind;        // RangeKind actually selected
 };
 // want = the preferred family (kRangePx: k_range_px at N = 8192, kRangeSeq: k_range_sq at N = 4096,
-// else k_range); window FMCW_WIN_Q15_RTL and spec (fmcw_spectrum_dtype) FMCW_SPEC_F16 / _S48 run
-// k_range (S48: N <= 1024 only, fn = nullptr otherwise)
+// else k_range); window FMCW_WIN_Q15_RTL and spec (fmcw_spectrum_dtype) FMCW_SPEC_F16 run k_range;
+// FMCW_SPEC_S48 runs the same family as fp32 (its quad form at T >= 4, pair form at T = 2)
 RangeInfo range_info(uint32_t n, int dtype, int window, int spec, int want);
 
 // ---- K2: Doppler window + FFT + |X| / NCI + map + 1-D CFAR --------------------------------
@@ -33,11 +33,12 @@ struct DopplerInfo {
 };
 DopplerFn doppler_fn_f32(uint32_t nc, int mti, bool fast, bool q15);  // inst_doppler.hip
 DopplerFn doppler_fn_f16(uint32_t nc, int mti, bool fast);            // inst_doppler_h16.hip
-DopplerFn doppler_fn_s48(uint32_t nc, int mti, bool fast);            // inst_doppler_s48.hip (nullptr: unsupported)
+// inst_doppler_s48.hip (nullptr: unsupported); pair = the S48 pair form (K1 tiles of T = 2 chirps)
+DopplerFn doppler_fn_s48(uint32_t nc, int mti, bool fast, bool pair);
 inline DopplerInfo doppler_info(uint32_t nc, int mti = FMCW_MTI_OFF, int spec = FMCW_SPEC_F32, bool fast = false,
-                                bool q15 = false) {
+                                bool q15 = false, int range_T = 4) {
   DopplerFn fn = spec == FMCW_SPEC_F16   ? doppler_fn_f16(nc, mti, fast)
-                 : spec == FMCW_SPEC_S48 ? doppler_fn_s48(nc, mti, fast)
+                 : spec == FMCW_SPEC_S48 ? doppler_fn_s48(nc, mti, fast, range_T == 2)
                                          : doppler_fn_f32(nc, mti, fast, q15);
   switch (nc) {
 #define D_(N) case N: return {fn, DopplerGeom<N>::WR, DopplerGeom<N>::NT};

@@ -392,11 +392,10 @@ int validate(const fmcw_config& c) {
   if (c.spectrum_dtype != FMCW_SPEC_F32 && c.spectrum_dtype != FMCW_SPEC_F16 && c.spectrum_dtype != FMCW_SPEC_S48)
     return fail(FMCW_EINVAL, "spectrum_dtype=%d unknown", c.spectrum_dtype);
   if (c.spectrum_dtype == FMCW_SPEC_S48) {
-    // one exponent per chirp quad of a range bin: the quad must be one K1 tile row (T >= 4 chirps:
-    // n_range <= 1024) and one K2 lane quad (n_doppler >= 64), and no MTI (the canceller reads
-    // neighbouring chirps from other lanes of the quad)
-    if (c.n_range > 1024 || c.n_doppler < 64)
-      return fail(FMCW_EINVAL, "spectrum_dtype S48 needs n_range <= 1024 and n_doppler >= 64");
+    // one exponent per chirp group of a range bin (a quad of a K1 tile row at n_range <= 1024, a
+    // pair above): the group must be one K2 lane group (n_doppler >= 64), and no MTI (the
+    // canceller reads neighbouring chirps from other lanes of the group)
+    if (c.n_doppler < 64) return fail(FMCW_EINVAL, "spectrum_dtype S48 needs n_doppler >= 64");
     if (c.mti_mode != FMCW_MTI_OFF || c.window == FMCW_WIN_Q15_RTL)
       return fail(FMCW_EINVAL, "spectrum_dtype S48 is defined with MTI off and an fp32 window (not Q15_RTL)");
   }
@@ -758,7 +757,7 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
                               : c.spectrum_dtype == FMCW_SPEC_S48 ? sizeof(S48)
                                                                   : sizeof(float2));
   occupancy_grid(ri.fn, ri.NT, 0, h->n_cu, &h->grid_range);
-  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype, h->k2_fast);
+  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype, h->k2_fast, false, ri.T);
   if (!ri.fn || !di.fn) {
     delete h;
     return fail(FMCW_EINVAL, "no kernel for this configuration (spectrum_dtype %d)", c.spectrum_dtype);
@@ -899,7 +898,7 @@ int fmcw_enqueue(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
   HIP_TRY(hipSetDevice(c.device_id));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const RangeInfo ri = range_info(c.n_range, c.in_dtype, c.window, c.spectrum_dtype, h->k1_want);
-  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype, h->k2_fast);
+  const DopplerInfo di = doppler_info(c.n_doppler, c.mti_mode, c.spectrum_dtype, h->k2_fast, false, ri.T);
   const size_t frame_px = (size_t)c.n_range * c.n_doppler;
   const size_t in_frame_bytes = cube_bytes(c, 1);
   const Cfar1DArgs cf1 = cfar1_args(c);

@@ -120,61 +120,92 @@ struct LoadI16 {
 // holding X / N_range (|X| <= N max|x| would overflow fp16 for ADC-scale input; the 2^-log2 N
 // scale is exact and K2 undoes it at load).
 // Spectrum formats (fmcw.h fmcw_spectrum_dtype): SP_F32 float2 (8 B), SP_F16 half2 of X / N (4 B),
-// SP_S48 (6 B, below).
-constexpr int SP_F32 = 0, SP_F16 = 1, SP_S48 = 2;
+// S48 (6 B, below) in its quad (SP_S48) or pair (SP_S48P) form.  K1 kernels take SP_S48 and pick
+// the form from their tile width T; K2 is instantiated per form.
+constexpr int SP_F32 = 0, SP_F16 = 1, SP_S48 = 2, SP_S48P = 3;
 struct __attribute__((packed)) S48 { uint16_t h[3]; };  // one S48 point: pointer steps of 6 B
 template <int SP> struct SpecEl { using T = float2; };
 template <> struct SpecEl<SP_F16> { using T = uint32_t; };
 template <> struct SpecEl<SP_S48> { using T = S48; };
+template <> struct SpecEl<SP_S48P> { using T = S48; };
 typedef _Float16 fmcw_h2 __attribute__((ext_vector_type(2)));
 
-// ---- S48: the corner-turned spectrum in 6 bytes per point, exact to 2^-23 of its chirp quad -----
-// The four chirps 4k .. 4k + 3 of one range bin (contiguous in a tile row: T >= 4) share one
-// exponent E = max frexp exponent of their 8 components (|x| < 2^E), clamped to >= -95; each
-// component is stored as q = rint(x 2^(22 - E)), a 23-bit two's-complement significand (clamped
-// to 2^22 - 1), so |x - q 2^(E - 22)| <= 2^(E - 23): 2^-23 of the quad's largest component (or of
-// 2^-95), where fp32 keeps 2^-24 of each.  Point record (48 bits, little-endian, point q of the
-// quad at bytes 6q .. 6q + 5): bits 0-22 re, 23-24 bits 2q, 2q + 1 of e8 = E + 127, 25-47 im.
-// K1 lanes hold chirp pairs (c0, c0 + 1), c0 even, and exchange the pair maximum with the lane of
-// the other pair of their quad (lane ^ 1); K2 lanes t .. t + 3 (P % 4 == 0) hold the quad's four
-// chirps and OR their 2-bit exponent pieces together across the quad (DPP).  Measured on the CPU
-// model (fp64 oracle, config-2 frames, per-bin error on bins >= 1e-3 of the frame peak): <= 3.3e-5
-// over 48 frames, against 1e-4 allowed; one exponent per point with 20-bit significands reached
-// 1.9e-4.
+// ---- S48: the corner-turned spectrum in 6 bytes per point, one exponent per chirp group --------
+// The G chirps Gk .. Gk + G - 1 of one range bin (contiguous in a tile row) share one exponent
+// E = max frexp exponent of their 2G components (|x| < 2^E), clamped to >= -95; each component is
+// stored as q = rint(x 2^(W - 1 - E)), a W-bit two's-complement significand (clamped to
+// 2^(W-1) - 1), so |x - q 2^(E - W + 1)| <= 2^(E - W): 2^-W of the group's largest component (or
+// of 2^-95), where fp32 keeps 2^-24 of each.  Two forms, by K1's tile width T:
+//   quad (T >= 4, n_range <= 1024): G = 4, W = 23, 2 exponent bits per point;
+//   pair (T = 2, n_range >= 2048):  G = 2, W = 22, 4 exponent bits per point.
+// Point record (48 bits, little-endian, point q of the group at bytes 6q .. 6q + 5): bits 0 .. W-1
+// re, then the 8/G bits (8/G) q .. of e8 = E + 127, then im in the top W bits.
+// K1 lanes hold chirp pairs (c0, c0 + 1), c0 even; in the quad form they exchange the pair maximum
+// with the lane of the other pair of their quad (lane ^ 1).  K2 lanes t .. t + G - 1 (P % G == 0)
+// hold the group's chirps and OR their exponent pieces together across it (DPP).  Measured on the
+// CPU model (fp64 oracle, per-bin error on bins >= 1e-3 of the frame peak): quad <= 3.3e-5 over 48
+// config-2 frames, pair 3.7e-8 at config 5 and 2.5e-8 at config 3, against 1e-4 allowed; one
+// exponent per point with 20-bit significands reached 1.9e-4 at config 2.
 typedef uint32_t fmcw_u3v __attribute__((ext_vector_type(3)));
-__device__ __forceinline__ fmcw_u3v s48_pack_pair(float2 v0, float2 v1, int q0) {
-  const float m = fmaxf(fmaxf(fabsf(v0.x), fabsf(v0.y)), fmaxf(fabsf(v1.x), fabsf(v1.y)));
-  const int el = __builtin_amdgcn_frexp_expf(m);  // m < 2^el (0 for m = 0)
-  const int ep = __builtin_amdgcn_mov_dpp(el, 0xB1 /* quad_perm [1,0,3,2]: lane ^ 1 */, 0xf, 0xf, false);
-  const int E = max(max(el, ep), -95);  // K2's scale 2^(E - 31) stays a normal float
+template <int G>
+__device__ __forceinline__ fmcw_u3v s48_pack(float2 v0, float2 v1, int q0) {
+  static_assert(G == 2 || G == 4, "pair or quad");
+  constexpr int W = G == 4 ? 23 : 22, PB = 8 / G;
+  // the largest |component| by an integer max of the sign-cleared bits (finite values): fmaxf's
+  // operand canonicalisation became a late `v_max_f32 vX, |vY|, |vY|` that hipcc (ROCm 7.2) placed
+  // right after the previous element's dwordx3 store, overwriting that store's data VGPRs without
+  // the 2 wait states the hazard needs -- intermittently corrupt tiles (tools/store_hazard_scan.py)
+  constexpr uint32_t AB = 0x7fffffffu;
+  const uint32_t mb = max(max(__float_as_uint(v0.x) & AB, __float_as_uint(v0.y) & AB),
+                          max(__float_as_uint(v1.x) & AB, __float_as_uint(v1.y) & AB));
+  int el = __builtin_amdgcn_frexp_expf(__uint_as_float(mb));  // max < 2^el (0 for 0)
+  if constexpr (G == 4) el = max(el, __builtin_amdgcn_mov_dpp(el, 0xB1 /* quad_perm [1,0,3,2]: lane ^ 1 */, 0xf, 0xf, false));
+  const int E = max(el, -95);  // K2's scale 2^(E - 31) stays a normal float
   const uint32_t e8 = (uint32_t)(E + 127);
-  const int sh = 22 - E;
+  const int sh = W - 1 - E;
+  // |x| < 2^E, so -2^(W-1) <= q <= 2^(W-1): only the top can leave the W-bit range (clamped)
   auto sig = [sh](float x) -> uint32_t {
     const int q = (int)__builtin_rintf(__builtin_amdgcn_ldexpf(x, sh));
-    return (uint32_t)min(max(q, -(1 << 22)), (1 << 22) - 1);
+    return (uint32_t)min(q, (1 << (W - 1)) - 1);
   };
   const uint32_t r0 = sig(v0.x), i0 = sig(v0.y), r1 = sig(v1.x), i1 = sig(v1.y);
-  const uint32_t b0 = (e8 >> (2 * q0)) & 3u, b1 = (e8 >> (2 * q0 + 2)) & 3u;
-  constexpr uint32_t M23 = (1u << 23) - 1;
+  constexpr uint32_t PM = (1u << PB) - 1;
+  const uint32_t b0 = (e8 >> (PB * q0)) & PM, b1 = (e8 >> (PB * q0 + PB)) & PM;
+  constexpr uint32_t MW = (1u << W) - 1;
   fmcw_u3v w;
-  w.x = (r0 & M23) | (b0 << 23) | (i0 << 25);                                // P0 bits 0-31
-  w.y = ((i0 >> 7) & 0xffffu) | (r1 << 16);                                  // P0 32-47, P1 0-15
-  w.z = ((r1 >> 16) & 0x7fu) | (b1 << 7) | (i1 << 9);                        // P1 16-47
+  w.x = (r0 & MW) | (b0 << W) | (i0 << (W + PB));                                   // P0 bits 0-31
+  w.y = ((i0 >> (32 - W - PB)) & 0xffffu) | (r1 << 16);                             // P0 32-47, P1 0-15
+  w.z = ((r1 >> 16) & ((1u << (W - 16)) - 1)) | (b1 << (W - 16)) | (i1 << (W - 16 + PB));  // P1 16-47
   return w;
 }
+// A 12-byte S48 store, padded: a VALU write of a wide store's data VGPRs within 2 wait states of
+// the store corrupts the stored data under load, and hipcc (ROCm 7.2, gfx950) pads that hazard
+// only for stores whose soffset is not an SGPR -- k_range_px's S48 tile stores (SGPR soffset) came
+// out with the next element's packing writing into the previous store's data VGPRs at once, and
+// the first frame of multi-group launches read back wrong under load (tools/store_hazard_scan.py
+// finds such sequences in a .s).  The two wait states are placed here, fenced against scheduling.
+template <int AUX>
+__device__ __forceinline__ void store_b96_padded(fmcw_u3v w, __amdgpu_buffer_rsrc_t rs, uint32_t vo, uint32_t so) {
+  __builtin_amdgcn_raw_buffer_store_b96(w, rs, vo, so, AUX);
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 1");
+  __builtin_amdgcn_sched_barrier(0);
+}
 // One point from the 8 bytes loaded at its record's byte offset rounded down to 4 (odd = its point
-// index is odd: the record starts at byte 2 of them); q2 = 2 (c & 3).  Every lane of the quad must
-// call it together.  Two byte permutes give the record's bits 0-31 and 16-47; the significands
-// land in the top 23 bits of a word (low bits zero), so v_cvt_f32_i32 reads q 2^9 exactly and one
-// packed multiply by 2^(E - 31) scales both components.
-__device__ __forceinline__ float2 s48_unpack(fmcw_u2v raw, uint32_t odd, uint32_t q2) {
+// index is odd: the record starts at byte 2 of them); qs = (8/G) (c % G), the shift of its exponent
+// piece.  Every lane of the group must call it together.  Two byte permutes give the record's bits
+// 0-31 and 16-47; the significands land in the top W bits of a word (low bits zero), so
+// v_cvt_f32_i32 reads q 2^(32-W) exactly and one packed multiply by 2^(E - 31) scales both.
+template <int G>
+__device__ __forceinline__ float2 s48_unpack(fmcw_u2v raw, uint32_t odd, uint32_t qs) {
+  constexpr int W = G == 4 ? 23 : 22, PB = 8 / G;
   const uint32_t so = odd * 0x02020202u;
   const uint32_t w0 = __builtin_amdgcn_perm(raw.y, raw.x, 0x03020100u + so);  // record bits 0-31
   const uint32_t w1 = __builtin_amdgcn_perm(raw.y, raw.x, 0x05040302u + so);  // record bits 16-47
-  const float re = (float)(int)(w0 << 9), im = (float)(int)(w1 & 0xfffffe00u);
-  int e = (int)(__builtin_amdgcn_ubfe(w0, 23, 2) << q2);
+  const float re = (float)(int)(w0 << (32 - W)), im = (float)(int)(w1 & ~((1u << (32 - W)) - 1));
+  int e = (int)(__builtin_amdgcn_ubfe(w0, W, PB) << qs);
   e |= __builtin_amdgcn_mov_dpp(e, 0xB1 /* lane ^ 1 */, 0xf, 0xf, false);
-  e |= __builtin_amdgcn_mov_dpp(e, 0x4E /* quad_perm [2,3,0,1]: lane ^ 2 */, 0xf, 0xf, false);
+  if constexpr (G == 4) e |= __builtin_amdgcn_mov_dpp(e, 0x4E /* quad_perm [2,3,0,1]: lane ^ 2 */, 0xf, 0xf, false);
   const float sc = __uint_as_float((uint32_t)(e - 31) << 23);  // 2^(E - 31), E = e - 127 >= -95
   typedef float f2v __attribute__((ext_vector_type(2)));
   const f2v r = f2v{re, im} * f2v{sc, sc};
@@ -185,6 +216,31 @@ __device__ __forceinline__ float2 s48_unpack(fmcw_u2v raw, uint32_t odd, uint32_
 template <bool NT>
 __device__ __forceinline__ fmcw_u2v ld_s48_raw(const S48* p, uint32_t odd) {
   return ld_u2<NT>(reinterpret_cast<const char*>(p) - 2 * odd);
+}
+// Pair form: both lanes of a pair load the pair's whole 12-byte element (from its 4-aligned start,
+// byte 6 p - 6 (p & 1)) and decode their own point with both exponent nibbles at hand -- no lane
+// exchange, and every load starts on the element (the 8-byte record loads of the quad form start
+// mid-element for odd points).
+__device__ __forceinline__ fmcw_u3v ld_s48_pair(const S48* p, uint32_t odd) {
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(p) - 6 * odd);
+  fmcw_u3v w;
+  w.x = q[0];
+  w.y = q[1];
+  w.z = q[2];
+  return w;
+}
+__device__ __forceinline__ float2 s48p_unpack(fmcw_u3v w, uint32_t odd) {
+  constexpr int W = 22;
+  const uint32_t lo = odd ? w.y : w.x, hi = odd ? w.z : w.y;  // the point's record: bytes 2 odd .. of {lo, hi}
+  const uint32_t so = odd * 0x02020202u;
+  const uint32_t w0 = __builtin_amdgcn_perm(hi, lo, 0x03020100u + so);  // record bits 0-31
+  const uint32_t w1 = __builtin_amdgcn_perm(hi, lo, 0x05040302u + so);  // record bits 16-47
+  const float re = (float)(int)(w0 << (32 - W)), im = (float)(int)(w1 & ~((1u << (32 - W)) - 1));
+  const uint32_t e = __builtin_amdgcn_ubfe(w.x, W, 4) | (__builtin_amdgcn_ubfe(w.z, W - 16, 4) << 4);
+  const float sc = __uint_as_float((e - 31) << 23);  // 2^(E - 31)
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  const f2v r = f2v{re, im} * f2v{sc, sc};
+  return make_float2(r.x, r.y);
 }
 
 __device__ __forceinline__ uint32_t pack_h2(float x, float y) {
@@ -233,7 +289,7 @@ template <int N> struct RangeGeom {
 // ROM integers c[n] (exact in fp32) and each sample is windowed as sat16((x c + 2^14) >> 14)
 // (window_multiplier.vhd:146-158) before it becomes fp32.
 // SP = spectrum format: SP_F16 (FMCW_SPEC_F16) tiles hold half2(X / N) (8-B stores of two chirps),
-// SP_S48 (FMCW_SPEC_S48, T >= 4) two 6-B S48 points (12-B stores).
+// SP_S48 (FMCW_SPEC_S48) two 6-B S48 points (12-B stores; the quad form at T >= 4, pair at T = 2).
 template <int N, typename LD, bool Q15 = false, int SP = SP_F32>
 __global__ void __launch_bounds__(RangeGeom<N>::NT)
 __attribute__((amdgpu_waves_per_eu(1)))
@@ -367,10 +423,8 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
       }
       if constexpr (SP == SP_F16) dst16[i * dstep / 2] = make_uint2(pack_h2(v0.x, v0.y), pack_h2(v1.x, v1.y));
       else if constexpr (SP == SP_S48) {
-        static_assert(T >= 4, "S48 shares an exponent over 4 chirps of a tile row");
-        __builtin_amdgcn_raw_buffer_store_b96(s48_pack_pair(v0, v1, c0 & 3), wrs,
-                                              (uint32_t)((dbase + i * dstep) * sizeof(S48)), 0,
-                                              kK1WriteThrough ? 16 /* sc1 */ : 0);
+        store_b96_padded<kK1WriteThrough ? 16 /* sc1 */ : 0>(s48_pack<T >= 4 ? 4 : 2>(v0, v1, c0 & (T >= 4 ? 3 : 0)),
+                                                            wrs, (uint32_t)((dbase + i * dstep) * sizeof(S48)), 0);
       }
       else if constexpr (kK1WriteThrough && N <= 4096) st_f4_wt(wrs, (uint32_t)((dbase + i * dstep) * sizeof(float2)), make_float4(v0.x, v0.y, v1.x, v1.y));
       else st_f4<kNtSpecSt>(dst + i * dstep, make_float4(v0.x, v0.y, v1.x, v1.y));
@@ -405,7 +459,7 @@ template <int N, int V> struct SqGeom {
   static constexpr int REG = padded(N);
   static constexpr int WAVES = V == 16 ? 4 : 2;  // per SIMD: 16 (V = 16) or 8 (V = 32) waves per CU
 };
-template <int N, typename LD, int V, int E, int W = SqGeom<N, V>::WAVES>
+template <int N, typename LD, int V, int E, int W = SqGeom<N, V>::WAVES, int SP = SP_F32>
 __global__ void __launch_bounds__(N / V) __attribute__((amdgpu_waves_per_eu(W)))
 k_range_sq(const void* __restrict__ cube, float2* __restrict__ inter, const float* __restrict__ win,
            const float* __restrict__ chirp_w, int nc, int n_groups, float /* q15_scale */, uint32_t* /* status */) {
@@ -496,19 +550,26 @@ k_range_sq(const void* __restrict__ cube, float2* __restrict__ inter, const floa
     // at N <= 4096 as k_range: no dirty spectrum lines left in L2 for the end-of-kernel release
     // (config 3: K1 58.3-58.7 -> 57.2-57.6 us per launch, 21.7-21.8 k -> 22.0-22.1 k frames/s,
     // profiles/r04/k1/policy/; nt + sc1 7 % slower)
+    // (SP_S48: the pair form, 12 B per element, same policy)
     const int t = opaque(t0);
     const size_t fbase = (size_t)fr * N * nc;
     constexpr bool WT = kK1WriteThrough && N <= 4096;
-    const __amdgpu_buffer_rsrc_t srs = wt_rsrc(inter + fbase, 0xffffffffu);  // one frame's tiles < 4 GiB
+    constexpr size_t EB = SP == SP_S48 ? sizeof(S48) : sizeof(float2);  // bytes per point
+    const __amdgpu_buffer_rsrc_t srs =  // one frame's tiles < 4 GiB
+        SP == SP_S48 ? wt_rsrc(reinterpret_cast<char*>(inter) + fbase * EB, 0xffffffffu) : wt_rsrc(inter + fbase, 0xffffffffu);
 #pragma unroll
     for (int gg = 0; gg < GF; ++gg)
 #pragma unroll
       for (int m = 0; m < RF; ++m) {
         const int d = t + P * gg + LL * m;
         const size_t off = ((size_t)(d / RB) * ncb + cb) * (RB * T) + (size_t)(d % RB) * T;
-        const float4 x = make_float4(X[0][gg][m].x, X[0][gg][m].y, X[1][gg][m].x, X[1][gg][m].y);
-        if constexpr (WT) st_f4_wt(srs, (uint32_t)(off * sizeof(float2)), x);
-        else st_f4<kNtSpecSt>(inter + fbase + off, x);
+        if constexpr (SP == SP_S48) {
+          store_b96_padded<WT ? 16 /* sc1 */ : 0>(s48_pack<2>(X[0][gg][m], X[1][gg][m], 0), srs, (uint32_t)(off * EB), 0);
+        } else {
+          const float4 x = make_float4(X[0][gg][m].x, X[0][gg][m].y, X[1][gg][m].x, X[1][gg][m].y);
+          if constexpr (WT) st_f4_wt(srs, (uint32_t)(off * sizeof(float2)), x);
+          else st_f4<kNtSpecSt>(inter + fbase + off, x);
+        }
       }
   }
 }
@@ -549,7 +610,7 @@ __device__ __forceinline__ void swap32(float2& a, float2& b) {
 // a vector-memory op issued after the group's 16 tile stores -- makes the next group's pass A wait,
 // in vmcnt order, for every one of those stores.  68 + 2 WS KiB of LDS per workgroup: two still fit
 // a CU (160 KiB) up to WS = 6.
-template <typename LD, int W = 4, int WS = 4>
+template <typename LD, int W = 4, int WS = 4, int SP = SP_F32>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(W)))
 k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const float* __restrict__ win,
            const float* __restrict__ chirp_w, int nc, int n_groups, float /* q15_scale */, uint32_t* /* status */) {
@@ -672,20 +733,28 @@ k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const floa
     }
     // tile stores: lane holds X[d] of both chirps for d = p (register m + 8) and p + 4096 (m)
     // d / 64 = (w >> 1) + 4 m' + 64 s, d % 64 = (l & 31) + 32 (w & 1); tile (d / 64, cb) is 1 KiB
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(inter + (size_t)fr * N * nc, (short)0, N * nc * 8, 0x00020000);
+    // (SP_S48: the pair form, 12-B elements in 768-B tiles)
+    constexpr int EB = SP == SP_S48 ? 2 * (int)sizeof(S48) : 16;  // bytes per (chirp 0, chirp 1) element
+    void* const fbase = SP == SP_S48 ? static_cast<void*>(reinterpret_cast<char*>(inter) + (size_t)fr * N * nc * (EB / 2))
+                                     : static_cast<void*>(inter + (size_t)fr * N * nc);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(fbase, (short)0, N * nc * (EB / 2), 0x00020000);
     const int t = opaque(t0);
     const int l = t & 63, w = t >> 6;
-    const int vo = (((w >> 1) + 32 * (1 - (l >> 5))) * ncb + cb) * 1024 + ((l & 31) + 32 * (w & 1)) * 16;
+    const int vo = (((w >> 1) + 32 * (1 - (l >> 5))) * ncb + cb) * (64 * EB) + ((l & 31) + 32 * (w & 1)) * EB;
 #pragma unroll
     for (int m = 0; m < 8; ++m)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int r = s ? m : m + 8;
-        typedef float f4v __attribute__((ext_vector_type(4)));
-        const f4v x = {X[0][r].x, X[0][r].y, X[1][r].x, X[1][r].y};
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(fmcw_u4v, x), rs, vo, (4 * m + 64 * s) * ncb * 1024,
-                                               0 /* write-back */);
+        if constexpr (SP == SP_S48) {
+          store_b96_padded<0 /* write-back */>(s48_pack<2>(X[0][r], X[1][r], 0), rs, (uint32_t)vo,
+                                               (4 * m + 64 * s) * ncb * (64 * EB));
+        } else {
+          typedef float f4v __attribute__((ext_vector_type(4)));
+          const f4v x = {X[0][r].x, X[0][r].y, X[1][r].x, X[1][r].y};
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(fmcw_u4v, x), rs, vo,
+                                                 (4 * m + 64 * s) * ncb * (64 * EB), 0 /* write-back */);
+        }
       }
   }
 }
@@ -1336,7 +1405,8 @@ constexpr int k2_waves() { return (FAST && MTI == 0 && NC == 256) ? 4 : 2; }
 // and the 1-D CFAR, when enabled, at the reference geometry (8 refs / 2 guards per side, need =
 // n_ref - rank <= 4, fp32 compare).  The generic kernel keeps those as uniform runtime branches,
 // whose other arms held registers and SGPRs (spills to VGPR lanes) across the tile loop.
-// SP: the spectrum format K1 wrote (SP_F32, SP_F16, SP_S48; S48 with MTI off, P % 4 == 0 and T >= 4).
+// SP: the spectrum format K1 wrote (SP_F32, SP_F16, SP_S48 quad form (T >= 4, P % 4 == 0), SP_S48P
+// pair form (T = 2, P % 2 == 0); S48 with MTI off).
 template <int NC, int MTI, int SP = SP_F32, bool FAST = false>
 __global__ void __launch_bounds__(DopplerGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(k2_waves<NC, MTI, FAST>())))
 k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, int ns, int nrx,
@@ -1354,11 +1424,13 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
   using SE = typename SpecEl<SP>::T;
   const SE* const inter = reinterpret_cast<const SE*>(inter_in);
   const float sscale = SP == SP_F16 ? (float)ns : 1.f;  // undoes K1's 1 / N_range of an fp16 spectrum
-  static_assert(SP != SP_S48 || (MTI == 0 && P % 4 == 0), "S48: a lane quad holds a chirp quad");
-  // S48: this lane's chirps c = t + P m all sit at c & 3 = t & 3 of their quad (t = lane % P);
+  constexpr bool S48F = SP == SP_S48 || SP == SP_S48P;
+  constexpr int SG = SP == SP_S48 ? 4 : 2;  // S48 exponent group: chirps per shared exponent
+  static_assert(!S48F || (MTI == 0 && P % SG == 0), "S48: a lane group holds a chirp group");
+  // S48: this lane's chirps c = t + P m all sit at c % G = t % G of their group (t = lane % P);
   // the two lane constants are derived from t where they are used (not held across the loop)
   auto s48_sh = [](int tt) { return (uint32_t)(tt & 1) << 4; };   // byte offset x 8 of the record in its load
-  auto s48_q2 = [](int tt) { return (uint32_t)(tt & 3) << 1; };
+  auto s48_qs = [](int tt) { return (uint32_t)(tt & (SG - 1)) * (8 / SG); };  // its exponent piece's shift
   const int rr = lane0 / P;
   const int t0 = lane0 % P;
   float* const mags = lds + wv * Gm::WFL;
@@ -1418,7 +1490,8 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
     return inter + ((size_t)fu * nrx + rx) * (size_t)ns * NC +
            off_of((uint32_t)(ru >> lgRB) << lgncb, (uint32_t)(ru & ((1 << lgRB) - 1)), 0);
   };
-  float2 nxt[PF ? NPF : 1];
+  using PfT = std::conditional_t<SP == SP_S48P, fmcw_u3v, float2>;  // a prefetched point (raw for S48)
+  PfT nxt[PF ? NPF : 1];
   const __amdgpu_buffer_rsrc_t srs = wt_rsrc(const_cast<SE*>(inter), 0xffffffffu);  // the prefetch's buffer loads
   // last-pass twiddle bases, once per lane (NC = 256: pass 1 + one radix-16 pass, k = t)
   constexpr bool TWH = NC / 16 <= 16 && P % 16 == 0;
@@ -1439,7 +1512,13 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
           const uint32_t sb = S * (uint32_t)sizeof(SE);
 #pragma unroll
           for (int m = 0; m < NPF; ++m) {
-            if constexpr (SP == SP_S48) {
+            if constexpr (SP == SP_S48P) {
+              // the point's whole pair element (decoded at use)
+              const uint32_t vo = (uint32_t)((const char*)pb - (const char*)inter) - 6u * ((uint32_t)tq & 1u);
+              nxt[m] = __builtin_bit_cast(fmcw_u3v, __builtin_amdgcn_raw_buffer_load_b96(srs, vo, so, kNtSpecLd ? 2 /* nt */ : 0));
+              so += sb;
+              asm volatile("" : "+s"(so));
+            } else if constexpr (S48F) {
               // the raw 8 bytes at the point's record rounded down to 4 (decoded at use)
               const uint32_t vo = (uint32_t)((const char*)pb - (const char*)inter) - (s48_sh(tq) >> 3);
               typedef float f2v __attribute__((ext_vector_type(2)));
@@ -1467,7 +1546,9 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
           for (int m = 0; m < NPF; ++m) {
             const uint32_t c = (uint32_t)(tq + P * m);
             const SE* pc = p + ((((c >> lgT) << lgRB) << lgT) | (c & (uint32_t)(T - 1)));
-            if constexpr (SP == SP_S48) {
+            if constexpr (SP == SP_S48P) {
+              nxt[m] = ld_s48_pair(pc, (uint32_t)tq & 1u);
+            } else if constexpr (S48F) {
               const fmcw_u2v r = ld_s48_raw<kNtSpecLd>(pc, (uint32_t)tq & 1u);
               nxt[m] = make_float2(__uint_as_float(r.x), __uint_as_float(r.y));
             } else {
@@ -1481,7 +1562,8 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
   // XCD-contiguous ids only where a workgroup reads less than a 128-B line of each tile
   // (measured: config 5 K2 177 -> 110 us per 4 frames; configs 2 / 3, whose workgroups read
   // whole lines, 2-3 % slower with it)
-  const bool xcd = ((WPB * WR * 8) << lgT) < 128;
+  // (S48: its 6-B points, so config 3's 96-B reads take the XCD mapping too)
+  const bool xcd = ((WPB * WR * (S48F ? 6 : 8)) << lgT) < 128;
   const int bid = xcd ? xcd_block_id((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
   prefetch(bid * WPB + wv, 0);
 
@@ -1505,17 +1587,39 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
     for (int rx = 0; rx < nrx; ++rx) {
       const SE* src = inter + ((size_t)f * nrx + rx) * (size_t)ns * NC;
       auto at = [&](uint32_t c) -> float2 {
-        if constexpr (SP == SP_S48) return s48_unpack(ld_s48_raw<kNtSpecLd>(src + off_of(rbase, rin, c), c & 1u), (uint32_t)t & 1u, s48_q2(t));
+        if constexpr (SP == SP_S48P) return s48p_unpack(ld_s48_pair(src + off_of(rbase, rin, c), c & 1u), (uint32_t)t & 1u);
+        else if constexpr (S48F) return s48_unpack<SG>(ld_s48_raw<kNtSpecLd>(src + off_of(rbase, rin, c), c & 1u), (uint32_t)t & 1u, s48_qs(t));
         else return ld_spec<kNtSpecLd>(src + off_of(rbase, rin, c), sscale);
       };
       float2 v[16];
+      // S48 pair form with a prefetch (NC = 512): the points not prefetched by buffer loads of the
+      // whole pair element, the lane's byte offset in a VGPR and the uniform m S part in the SGPR
+      // offset -- flat 64-bit addresses per point took 183 VGPRs (2 waves per SIMD) against fp32's
+      // 165 (3): config-3 K2 82 -> 60 us per 4-frame launch.  At NC = 1024 (no prefetch) the flat
+      // loads stay: with buffer loads the kernel needs 171 VGPRs, and held to 155 (3 waves) by
+      // loading 8 points at a time it waits 3x longer on them (SQ_WAIT_INST_ANY per frame 15.4 M vs
+      // fp32 5.3 M) and took 118 against 99-107 us per launch (profiles/r05/s48_pair/).
+      uint32_t p_vo = 0, p_sb = 0;
+      constexpr bool PBUF = SP == SP_S48P && NPF > 0;
+      if constexpr (PBUF) {
+        p_vo = (uint32_t)((const char*)(src + off_of(rbase, rin, (uint32_t)t)) - (const char*)inter) - 6u * ((uint32_t)t & 1u);
+        p_sb = ((uint32_t)(P >> lgT) << (lgRB + lgT)) * (uint32_t)sizeof(S48);
+      }
+      static_assert(!PBUF || P % 2 == 0, "pair form: chirps t + P m sit m S elements apart");
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int c = t + P * m;
         float2 x;
-        if (m < NPF) {
-          x = nxt[m < NPF ? m : 0];
-          if constexpr (SP == SP_S48) x = s48_unpack(fmcw_u2v{__float_as_uint(x.x), __float_as_uint(x.y)}, (uint32_t)t & 1u, s48_q2(t));
+        if (PBUF && m >= NPF) {
+          x = s48p_unpack(__builtin_bit_cast(fmcw_u3v, __builtin_amdgcn_raw_buffer_load_b96(srs, p_vo, (uint32_t)m * p_sb, 0)),
+                          (uint32_t)t & 1u);
+        } else if (m < NPF) {
+          if constexpr (SP == SP_S48P) {
+            x = s48p_unpack(nxt[m < NPF ? m : 0], (uint32_t)t & 1u);
+          } else {
+            x = nxt[m < NPF ? m : 0];
+            if constexpr (S48F) x = s48_unpack<SG>(fmcw_u2v{__float_as_uint(x.x), __float_as_uint(x.y)}, (uint32_t)t & 1u, s48_qs(t));
+          }
         } else {
           x = at((uint32_t)c);
         }

@@ -52,13 +52,43 @@ def test_library_exports_every_symbol(lib_built):
         assert getattr(lib_built, name) is not None
 
 
-def test_gfx950_code_object_present(lib_built):
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(L.LIB_PATH)],
-                         capture_output=True, text=True)
-    text = out.stdout + out.stderr
+OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+
+
+def extract_code_objects(tmp_path):
+    """The library's offload bundles, extracted from a copy (llvm-objdump --offloading writes them
+    next to its input)."""
+    import shutil
+    lib = tmp_path / "libfmcw.so"
+    shutil.copy(L.LIB_PATH, lib)
+    out = subprocess.run([OBJDUMP, "--offloading", str(lib)], capture_output=True, text=True, cwd=tmp_path)
+    return out.stdout + out.stderr, sorted(tmp_path.glob("libfmcw.so.*gfx950"))
+
+
+def test_gfx950_code_object_present(lib_built, tmp_path):
+    text, cos = extract_code_objects(tmp_path)
     if "gfx950" not in text:  # older objdump: fall back to the bundle id string
         data = L.LIB_PATH.read_bytes()
         assert b"gfx950" in data
+
+
+def test_no_wide_store_data_hazard(lib_built, tmp_path):
+    """No VALU write of a dwordx3/x4 store's data VGPRs within 2 wait states of the store in any
+    shipped kernel (tools/store_hazard_scan.py; hipcc leaves that hazard unpadded for stores with
+    an SGPR soffset, which corrupted S48 tiles intermittently before kernels.hpp store_b96_padded)."""
+    _, cos = extract_code_objects(tmp_path)
+    if not cos:
+        pytest.skip("this llvm-objdump cannot extract offload bundles")
+    dis = []
+    for co in cos:
+        d = tmp_path / (co.name + ".dis")
+        d.write_text(subprocess.run([OBJDUMP, "-d", "--mcpu=gfx950", str(co)], capture_output=True, text=True,
+                                    check=True).stdout)
+        dis.append(str(d))
+    from conftest import REPO
+    out = subprocess.run(["python3", str(REPO / "tools" / "store_hazard_scan.py"), *dis], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout[-2000:]
+    assert "0 unpadded" in out.stdout
 
 
 def test_struct_layouts():
@@ -216,14 +246,17 @@ def test_comm_check_verdict(lib_built):
     assert lib_built.fmcw_comm_fail_next_alloc_for_test(0) == L.FMCW_OK
 
 
-@pytest.mark.parametrize("field,value", [("n_range", 2048), ("n_range", 8192), ("n_doppler", 32),
-                                         ("mti_mode", 2)])
+@pytest.mark.parametrize("field,value", [("n_doppler", 32), ("mti_mode", 2), ("mti_mode", 3),
+                                         ("window", L.WIN_Q15_RTL)])
 def test_s48_spectrum_limits(lib_built, field, value):
-    """FMCW_SPEC_S48 shares an exponent over 4 chirps of a K1 tile row and a K2 lane quad:
-    n_range <= 1024, n_doppler >= 64, MTI off, fp32 window -- rejected at fmcw_create otherwise."""
+    """FMCW_SPEC_S48 shares an exponent over a chirp group of a K1 tile row (a quad at n_range <=
+    1024, a pair above) held by one K2 lane group: n_doppler >= 64, MTI off, fp32 window --
+    rejected at fmcw_create otherwise (any n_range is accepted)."""
     cfg = L.default_config()
     cfg.spectrum_dtype = L.SPEC_S48
     setattr(cfg, field, value)
+    if field == "window":
+        cfg.in_dtype = L.IN_I16  # the Q15 window's own requirement
     h = C.c_void_p()
     assert lib_built.fmcw_create(C.byref(cfg), C.byref(h)) == L.FMCW_EINVAL
     assert b"S48" in lib_built.fmcw_last_error()

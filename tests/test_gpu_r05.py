@@ -236,6 +236,12 @@ def test_comm_create_alloc_failure_one_rank(gpu):
     (512, 128, 4, "f32", "os2d", "two_targets"),       # T = 8
     (128, 1024, 3, "f32", "os2d", "random_target"),    # T = 16, NC = 1024 (no prefetch)
     (1024, 512, 3, "f32", "os1d", "random_target"),
+    # the pair form (K1 tiles of T = 2 chirps, n_range >= 2048): k_range, k_range_sq, k_range_px
+    (2048, 256, 3, "f32", "os1d", "random_target"),
+    (4096, 128, 2, "i16", "os2d", "two_targets"),
+    (4096, 64, 2, "f32", "os1d", "random_target"),     # P = 4
+    (8192, 64, 2, "f16", "os1d", "two_targets"),
+    (8192, 128, 2, "f32", "os2d", "random_target"),
 ])
 def test_s48_parity(gpu, ns, nc, nf, dtype, cfar, recipe):
     """Maps within the north star's 1e-4 (per frame and per bin above 1e-3 of the frame peak) of
@@ -284,3 +290,28 @@ def test_s48_bench_shape_two_chunks(gpu):
     for f in range(n_u, F):
         assert np.array_equal(rd_map[f], rd_map[f % n_u])
     np.testing.assert_array_equal(dets, CB.cfar(rd_map, O.Cfar1D(), threads=16, cap=1 << 22))
+
+
+@pytest.mark.parametrize("wl", ["c3", "c5"])
+def test_s48_bench_shape_parity(wl):
+    """Configs 3 and 5 at the bench's own shape (16 frames, one call) on the S48 spectrum in its
+    pair form: 48 MiB per frame, so the auto chunk takes 4 frames (16 = 4 x 4, no one-frame tail
+    launch).  Maps of the first and last frame within 1e-4 of the fp64 oracle, every detection
+    bit-exact vs the C oracle's 2-D OS-CFAR on the GPU's map (as test_gpu_r04's fp32 case)."""
+    import sys
+    if str(REPO) not in sys.path:
+        sys.path.insert(0, str(REPO))
+    import bench
+    from test_gpu_parity import to_complex
+    w = bench.WORKLOADS[wl]
+    F, ns, nc, nrx, dtype = w["frames"], w["ns"], w["nc"], w["nrx"], w["dtype"]
+    cube = synth.frames(F, ns, nc, nrx, w["recipe"], seed=1234, dtype=dtype)
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, N_RX=nrx, in_dtype=dtype, cfar=w["cfar"], max_frames=F,
+                   spectrum="s48") as core:
+        assert core.info("chunk") == 4
+        out = core.process(cube)
+    for f in (0, F - 1):
+        ref = O.process(to_complex(cube[f], dtype), None)["mag"]
+        check_map(out.rd_map[f:f + 1], ref[None])
+    np.testing.assert_array_equal(out.dets, CB.cfar(out.rd_map, O.Cfar2D(), threads=16))
+    assert set(out.dets["frame"].tolist()) == set(range(F))

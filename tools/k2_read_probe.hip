@@ -11,6 +11,11 @@
 //   pairs32    2 rows per wave, lanes 2k / 2k + 1 load rows r / r + 1 of one tile: 32 contiguous
 //              bytes per tile and instruction (a K2 that would hold chirp pairs per lane)
 //   linear16   the same bytes front to back, 16 B per lane (the streaming ceiling)
+//   s48_*      the S48 pair form (6-B points, 12-B chirp-pair elements, 768-B tiles), K2's rows8
+//              order over as many frames as fill the same bytes (4 for 3 fp32 frames):
+//              s48_x2 = 8 B per lane from the point's record rounded down to 4 (the quad form's
+//              load), s48_x3 = the pair's whole 12 B per lane, s48_2x1 = two aligned dword loads
+//              per lane, s48_x3w8 = s48_x3 with 8 waves (rows) per workgroup
 // usage: tools/k2_read_probe [frames=3] [reps=20]
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -98,6 +103,34 @@ __global__ void __launch_bounds__(256) k2_pairs32(const float4* __restrict__ s, 
   sink[blockIdx.x * 256 + threadIdx.x] = acc;
 }
 
+// S48 pair form: element (r, c) of one frame at byte 6 * off_of(r, c)
+template <int MODE, int W = 4>
+__global__ void __launch_bounds__(64 * W) k2_s48(const char* __restrict__ s, int rows, float* __restrict__ sink) {
+  const int b = xcd_id(blockIdx.x, gridDim.x);
+  const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const int row = b * W + w;
+  if (row >= rows) return;
+  const int f = row / NS, r = row % NS;
+  const char* p = s + (size_t)f * NS * NC * 6;
+  const int odd = t & 1;
+  uint32_t acc = 0;
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const char* e = p + 6 * off_of(r, t + 64 * m);
+    if constexpr (MODE == 0) {
+      const uint2 v = *reinterpret_cast<const uint2*>(e - 2 * odd);
+      acc += v.x ^ v.y;
+    } else if constexpr (MODE == 1) {
+      const uint32_t* q = reinterpret_cast<const uint32_t*>(e - 6 * odd);
+      acc += q[0] ^ q[1] ^ q[2];
+    } else {
+      const uint32_t* q = reinterpret_cast<const uint32_t*>(e - 2 * odd);
+      acc += q[0] ^ __builtin_nontemporal_load(q + 1);
+    }
+  }
+  sink[blockIdx.x * 64 * W + threadIdx.x] = (float)acc;
+}
+
 __global__ void __launch_bounds__(256) linear16(const float4* __restrict__ s, size_t n4, float* __restrict__ sink) {
   float acc = 0.f;
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
@@ -140,6 +173,14 @@ int main(int argc, char** argv) {
   run("rows8_w8nx", [&] { hipLaunchKernelGGL((k2_rows8w<8, 0>), dim3(rows / 8), dim3(512), 0, 0, s, rows, sink); });
   run("k2_rows16", [&] { hipLaunchKernelGGL(k2_rows16, dim3(g16), dim3(256), 0, 0, reinterpret_cast<const float4*>(s), rows, sink); });
   run("pairs32", [&] { hipLaunchKernelGGL(k2_pairs32, dim3(g16), dim3(256), 0, 0, reinterpret_cast<const float4*>(s), rows, sink); });
+  {
+    const int rows48 = (int)(bytes / (NS * NC * 6)) * NS;  // same bytes: 4 S48 frames per 3 fp32
+    const char* c = reinterpret_cast<const char*>(s);
+    run("s48_x2", [&] { hipLaunchKernelGGL((k2_s48<0>), dim3(rows48 / 4), dim3(256), 0, 0, c, rows48, sink); });
+    run("s48_x3", [&] { hipLaunchKernelGGL((k2_s48<1>), dim3(rows48 / 4), dim3(256), 0, 0, c, rows48, sink); });
+    run("s48_2x1", [&] { hipLaunchKernelGGL((k2_s48<2>), dim3(rows48 / 4), dim3(256), 0, 0, c, rows48, sink); });
+    run("s48_x3w8", [&] { hipLaunchKernelGGL((k2_s48<1, 8>), dim3(rows48 / 8), dim3(512), 0, 0, c, rows48, sink); });
+  }
   run("linear16", [&] { hipLaunchKernelGGL(linear16, dim3(glin), dim3(256), 0, 0, reinterpret_cast<const float4*>(s), bytes / 16, sink); });
   CHECK(hipGetLastError());
   CHECK(hipFree(s));
