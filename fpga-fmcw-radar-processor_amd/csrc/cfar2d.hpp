@@ -149,6 +149,8 @@ constexpr size_t cfar2d_smem_bytes(int hr) {
 // screen's LDS reads in flight ahead of the accumulation (round 5: 2 or 3 measured alike, 2 keeps
 // k_cfar2d_lv spill-free at 4 waves per SIMD)
 constexpr int kK3LvQA = 560, kK3LvQB = 680, kK3ScreenAhead = 2;
+// k_cfar2d: odd strips of a frame walk upwards (round 5; see the strip loop)
+constexpr bool kK3AltDir = true;
 // level nibbles of 4 cells from their key16 pairs (cells d, d + 1 | d + 2, d + 3): (k | 0x8000) - Q has
 // bit 15 set iff k >= Q (k < 0x8000, 1 <= Q <= 0x8000: no borrow across the halves); the byte
 // permute collects bits 15 / 31 of both words as bit 7 of 4 bytes
@@ -524,7 +526,15 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
     float4 pre[4];
     float pre4[4];
     uint32_t wa2 = 0u, wb2 = 0u;  // LV: the CUT bounds of the two levels (cfar2d_screen_lv)
-    for (int t = t_beg; t < t_end; ++t) {
+    // Odd strips of a frame walk upwards (kK3AltDir): the two strips on either side of a strip
+    // boundary then stage the halo rows they share at the same time -- at both strips' start or
+    // both strips' end -- and workgroups g and g + nf (neighbouring strips of one frame) sit on one
+    // XCD when nf % 8 == 0, so the second load of those rows hits its L2 (config 3: map traffic
+    // 1.125x -> 1.01x of the algorithmic bytes).
+    const bool up = kK3AltDir && ((g / nf) & 1);
+    for (int k = 0; k < t_end - t_beg; ++k) {
+      const int t = up ? t_end - 1 - k : t_beg + k;
+      const bool first = k == 0, last = k + 1 == t_end - t_beg;
       const int wt0 = t * WPB;                             // first wave tile of this step
       const int n_wt = min(WPB, wt_per_frame - wt0);
       const int r0 = wt0 * WR;                             // first CUT row of this step
@@ -533,7 +543,7 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
       const int d0 = (lane % TPR) * 16;
       const int r = r0 + rlw;
       __syncthreads();  // the previous step's waves are done with the rows and the lists
-      if (t == t_beg) {
+      if (first) {
         // rows r0-hr .. r0+TR+hr-1 (zero outside the map), 4 float4 loads in flight per lane: the
         // key16 rows first, then the strip's levels (or key base) from the staged keys of the first
         // step's CUT rows, then the screen rows from the keys
@@ -627,32 +637,34 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
           else put_scr(rr, x, d, pm_word(kw, (uint32_t)kr[4]));
         }
       } else {
-        // the ring turns by TR rows; the TR new rows (prefetched during the previous step) go
-        // into the slots of the TR rows that left
-        rr.base += TR;
+        // the ring turns by TR rows (downwards: tile row x moves to x - TR; upwards: to x + TR);
+        // the TR new rows (prefetched during the previous step) go into the slots of the TR rows
+        // that left, at the bottom (rows nr - TR ..) or the top (rows 0 .. TR - 1) of the tile
+        rr.base += up ? nr - TR : TR;
         if (rr.base >= nr) rr.base -= nr;
+        const int x0 = up ? 0 : nr - TR;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int e4 = tid + u * NT;
           const int i = e4 / (NC / 4), d = (e4 - i * (NC / 4)) * 4;
-          const uint2 kw = put_k16(rr, nr - TR + i, d, pre[u]);
+          const uint2 kw = put_k16(rr, x0 + i, d, pre[u]);
           if constexpr (LV) {
-            put_scr(rr, nr - TR + i, d, lv_nibbles(kw, qa2, qb2));
+            put_scr(rr, x0 + i, d, lv_nibbles(kw, qa2, qb2));
           } else {
             const float v4 = a.compat ? q17(pre4[u]) : nonneg(pre4[u]);
-            put_scr(rr, nr - TR + i, d, pm_word(kw, key16(v4)));
+            put_scr(rr, x0 + i, d, pm_word(kw, key16(v4)));
           }
         }
       }
-      if (t + 1 < t_end) {  // prefetch the next step's new rows r0 + TR + hr .. (zero past the map)
+      if (!last) {  // prefetch the next step's new rows: r0 + TR + hr .. or r0 - TR - hr .. (zero off the map)
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int e4 = tid + u * NT;
           const int i = e4 / (NC / 4), d = (e4 - i * (NC / 4)) * 4;
-          const int r = r0 + TR + a.hr + i;
+          const int r = (up ? r0 - TR - a.hr : r0 + TR + a.hr) + i;
           pre[u] = make_float4(0.f, 0.f, 0.f, 0.f);
           pre4[u] = 0.f;
-          if (r < ns) {
+          if (r >= 0 && r < ns) {
             pre[u] = *reinterpret_cast<const float4*>(fm + (size_t)r * NC + d);
             if constexpr (!LV) pre4[u] = fm[(size_t)r * NC + ((d + 4) & (NC - 1))];
           }
@@ -1010,7 +1022,10 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
     const float* fm = map + (size_t)f * ns * NC;
     int base = 0;  // ring slot of tile row 0
     float4 pre[4];
-    for (int t = t_beg; t < t_end; ++t) {
+    const bool up = kK3AltDir && ((g / nf) & 1);  // odd strips walk upwards, as k_cfar2d's
+    for (int k = 0; k < t_end - t_beg; ++k) {
+      const int t = up ? t_end - 1 - k : t_beg + k;
+      const bool first = k == 0, last = k + 1 == t_end - t_beg;
       const int wt0 = t * WPB;
       const int n_wt = min(WPB, wt_per_frame - wt0);
       const int r0 = wt0 * WR;
@@ -1018,7 +1033,7 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
       const int d0 = (lane % TPR) * 16;
       const int r = r0 + rlw;
       __syncthreads();  // the previous step's waves are done with the rows
-      if (t == t_beg) {
+      if (first) {
         // levels: the mean key7 level of the first step's CUT rows (this thread's 16 cells), then the
         // kK3LvQA / _QB quantiles of a 128-bin histogram around it
         float4 v[4];
@@ -1108,25 +1123,27 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
           }
         }
       } else {
-        // the ring turns by TR rows; the TR new rows (prefetched) go into the slots of the rows that left
-        base += TR;
+        // the ring turns by TR rows; the TR new rows (prefetched) go into the slots of the rows that
+        // left: tile rows NR - TR .. (downwards) or 0 .. TR - 1 (upwards)
+        base += up ? NR - TR : TR;
         if (base >= NR) base -= NR;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           int i, d;
           blk(u, i, d);
-          int x = NR - TR + i + base;
+          int x = (up ? 0 : NR - TR) + i + base;
           x = x >= NR ? x - NR : x;
           put(x, d, pre[u]);
         }
       }
-      if (t + 1 < t_end) {  // prefetch the next step's new rows r0 + TR + hr .. (zero past the map)
+      if (!last) {  // prefetch the next step's new rows: r0 + TR + hr .. or r0 - TR - hr .. (zero off the map)
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           int i, d;
           blk(u, i, d);
-          const int rr = r0 + TR + HR + i;
-          pre[u] = rr < ns ? *reinterpret_cast<const float4*>(fm + (size_t)rr * NC + d) : make_float4(0.f, 0.f, 0.f, 0.f);
+          const int rr = (up ? r0 - TR - HR : r0 + TR + HR) + i;
+          pre[u] = rr >= 0 && rr < ns ? *reinterpret_cast<const float4*>(fm + (size_t)rr * NC + d)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
       __syncthreads();

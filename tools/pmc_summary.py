@@ -29,7 +29,7 @@ PATTERNS = {
     # K3 = the three launches of a 2-D CFAR batch (k_cfar2d, k_cfar2d_decide, k_cfar2d_emit; round 4)
     "c3": {"k_range": r"k_range\w*<4096,", "k_doppler": r"k_doppler<512,", "k_cfar": r"k_cfar2d(_decide|_emit)?<512[,>]"},
     "c5": {"k_range": r"k_range(\w*<8192,|_px<)", "k_doppler": r"k_doppler<1024,",
-           "k_cfar": r"k_cfar2d(_decide|_emit)?<1024[,>]"},
+           "k_cfar": r"k_cfar2d(_lv|_decide|_emit)?<1024[,>]"},
 }
 ALG = {  # algorithmic bytes per frame, fp32 spectrum
     "c2": {"k_range": 1024 * 256 * 16, "k_doppler": 1024 * 256 * 12},
