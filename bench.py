@@ -25,7 +25,7 @@ read 7-10 % low (profiles/r04/warmup/).  --prewarm-s 0 restores the W-only warm-
 roofline: the dominant kernel's algorithmic bytes per launch / its average launch duration,
 from HIP events the library records on the launch stream (fmcw_set_profiling: the dispatches'
 own begin / end timestamps, hipExtLaunchKernelGGL) over a profiled repeat of the timed steps.  traffic: HBM bytes per launch from rocprofv3 PMC passes
-(profiles/pmc_r04.json, per frame x the launch's mean frames; tools/pmc_summary.py), or null.
+(profiles/pmc_r05.json, per frame x the launch's mean frames; tools/pmc_summary.py), or null.
 The 2-D CFAR (k_cfar2d) is bound by VALU work, not bytes: its roofline is SQ_INSTS_VALU per
 launch (same profile file) / launch time against the chip's VALU issue rate (2 wave-instructions
 per CU per clock at 2.4 GHz), its map bytes beside.
@@ -44,7 +44,7 @@ sys.path.insert(0, str(REPO / "fpga-fmcw-radar-processor_amd"))
 
 HBM_PEAK_GBPS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CLOCK_GHZ = 2.4             # MI355X peak engine clock
-PMC_FILE = "pmc_r04.json"   # per-frame HBM bytes and SQ counts per workload (tools/pmc_summary.py)
+PMC_FILE = "pmc_r05.json"   # per-frame HBM bytes and SQ counts per workload (tools/pmc_summary.py)
 
 WORKLOADS = {
     "c2": dict(ns=1024, nc=256, nrx=1, dtype="f32", cfar="os1d", frames=1024, recipe="two_targets",
