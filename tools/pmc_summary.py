@@ -16,7 +16,7 @@ gfx950 correction: FETCH_SIZE reports half the bytes of a wide coalesced streami
 is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.  Units of both: KiB.
 
 usage: python tools/pmc_summary.py --fetch F.csv --write W.csv [--sq SQ.csv]
-       --frames c2=5120 --frames c3=80 --frames c5=80 --out profiles/pmc_r04.json
+       --frames c2=5120 --frames c3=80 --frames c5=80 --out profiles/pmc_r05.json
 """
 import argparse
 import collections
@@ -62,7 +62,7 @@ def main():
     ap.add_argument("--sq", default=None)
     ap.add_argument("--frames", action="append", default=[], help="workload=frames processed in the run")
     ap.add_argument("--command", default="python3 bench.py --steps 2 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-h2d")
-    ap.add_argument("--out", default="profiles/pmc_r04.json")
+    ap.add_argument("--out", default="profiles/pmc_r05.json")
     a = ap.parse_args()
     frames = {k: int(v) for k, v in (x.split("=") for x in a.frames)}
     tables = [read(a.fetch), read(a.write)] + ([read(a.sq)] if a.sq else [])
