@@ -47,11 +47,11 @@ CLOCK_GHZ = 2.4             # MI355X peak engine clock
 PMC_FILE = "pmc_r05.json"   # per-frame HBM bytes and SQ counts per workload (tools/pmc_summary.py)
 
 WORKLOADS = {
-    "c2": dict(ns=1024, nc=256, nrx=1, dtype="f32", cfar="os1d", frames=1024, recipe="two_targets",
+    "c2": dict(ns=1024, nc=256, nrx=1, dtype="f32", cfar="os1d", frames=1024, recipe="two_targets", spectrum="s48",
                desc="BASELINE config 2: 256 chirps x 1024 samples fp32, 1 Rx, OS-CFAR 1-D 16 ref / 4 guard"),
-    "c3": dict(ns=4096, nc=512, nrx=4, dtype="f32", cfar="os2d", frames=16, recipe="two_targets",
+    "c3": dict(ns=4096, nc=512, nrx=4, dtype="f32", cfar="os2d", frames=16, recipe="two_targets", spectrum="f32",
                desc="BASELINE config 3: 512 chirps x 4096 samples fp32, 4 Rx NCI, 2-D OS-CFAR"),
-    "c5": dict(ns=8192, nc=1024, nrx=1, dtype="f16", cfar="os2d", frames=16, recipe="two_targets",
+    "c5": dict(ns=8192, nc=1024, nrx=1, dtype="f16", cfar="os2d", frames=16, recipe="two_targets", spectrum="f32",
                desc="BASELINE config 5: 1024 chirps x 8192 range bins, fp16 complex samples, 2-D OS-CFAR"),
 }
 SUB = {"c3": "config3", "c5": "config5"}
@@ -74,8 +74,10 @@ def parse():
     ap.add_argument("--gather", default="rccl", choices=["rccl", "torch"],
                     help="N > 1: libfmcw's RCCL gather-to-root (no host sync) or torch all_gather")
     ap.add_argument("--no-h2d", action="store_true", help="skip the H2D-inclusive measurement")
-    ap.add_argument("--spectrum", default="f32", choices=["f32", "f16", "s48"],
-                    help="element type of the corner-turned spectrum (fmcw.h fmcw_spectrum_dtype)")
+    ap.add_argument("--spectrum", default=None, choices=["f32", "f16", "s48"],
+                    help="element type of the corner-turned spectrum (fmcw.h fmcw_spectrum_dtype); default: "
+                         "the workload's (WORKLOADS: s48 at config 2, where A/B measured it faster, f32 at "
+                         "configs 3 / 5, where it was not)")
     return ap.parse_args()
 
 
@@ -139,6 +141,20 @@ def kernel_rooflines(wl, name, F, steps, kt, spectrum, n_cu, pmc):
     return out
 
 
+SPECTRUM_FORMAT = {  # fmcw.h fmcw_spectrum_dtype; every arithmetic step is fp32 either way
+    "f32": "complex fp32, 8 B per point",
+    "f16": "half2 of X / N_range, 4 B per point (map within 2e-3)",
+    "s48": "6 B per point: 23-bit significands sharing an 8-bit exponent per chirp quad of a range bin "
+           "(22-bit per pair above n_range 1024); map within the north star's 1e-4 of the fp64 oracle (tested)",
+}
+
+
+def spectrum_of(wl, args, primary):
+    """The corner-turned spectrum format a workload runs: --spectrum for the primary workload if
+    given, else the workload's own (WORKLOADS)."""
+    return args.spectrum if primary and args.spectrum else wl["spectrum"]
+
+
 def run_workload(name, args, world, rank, dev, primary, pmc, n_cu):
     import numpy as np
     import torch
@@ -154,7 +170,7 @@ def run_workload(name, args, world, rank, dev, primary, pmc, n_cu):
     local = dev.index
     core = RadarCore(N_RANGE=ns, N_DOPPLER=nc, N_RX=nrx, in_dtype=wl["dtype"], cfar=wl["cfar"],
                      max_frames=F, chunk_frames=args.chunk if primary else 0, device=local,
-                     spectrum=args.spectrum if primary else "f32")
+                     spectrum=spectrum_of(wl, args, primary))
     # synthetic input: 16 distinct frames (seed 1234 + global frame), tiled to F, resident in HBM
     n_u = min(16, F)
     first_global = rank * F
@@ -286,7 +302,7 @@ def run_workload(name, args, world, rank, dev, primary, pmc, n_cu):
     elapsed_prof = timed(steps)
     kt = core.kernel_times()
     core.set_profiling(False)
-    spectrum = args.spectrum if primary else "f32"
+    spectrum = spectrum_of(wl, args, primary)
     kern = kernel_rooflines(wl, name, F, steps, kt, spectrum, n_cu, pmc)
     dom = max((k for k in kern if k in ("k_range", "k_doppler", "k_cfar")), key=lambda k: kern[k]["ms_per_step"])
     value = world * F * steps / elapsed
@@ -301,6 +317,7 @@ def run_workload(name, args, world, rank, dev, primary, pmc, n_cu):
         "config": {"workload": wl["desc"], "frames_per_gpu_step": F, "n_chirps": nc,
                    "n_samples": ns, "n_rx": nrx, "cfar": wl["cfar"], "rd_map": "linear fp32, written",
                    "spectrum": spectrum,
+                   "spectrum_format": SPECTRUM_FORMAT[spectrum],
                    "detection_gather": gather_kind if gather else "none",
                    "parallelism": f"frame-sharded x{world}"},
         "range_kernel": core.info("range_kernel"),

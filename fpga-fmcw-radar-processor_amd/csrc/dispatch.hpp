@@ -21,7 +21,8 @@ struct RangeInfo {
 };
 // want = the preferred family (kRangePx: k_range_px at N = 8192, kRangeSeq: k_range_sq at N = 4096,
 // else k_range); window FMCW_WIN_Q15_RTL and spec (fmcw_spectrum_dtype) FMCW_SPEC_F16 run k_range;
-// FMCW_SPEC_S48 runs the same family as fp32 (its quad form at T >= 4, pair form at T = 2)
+// FMCW_SPEC_S48 runs the same family as fp32 (quad form at T >= 8, strided quads at T = 4, pair
+// form at T = 2)
 RangeInfo range_info(uint32_t n, int dtype, int window, int spec, int want);
 
 // ---- K2: Doppler window + FFT + |X| / NCI + map + 1-D CFAR --------------------------------
@@ -33,12 +34,14 @@ struct DopplerInfo {
 };
 DopplerFn doppler_fn_f32(uint32_t nc, int mti, bool fast, bool q15);  // inst_doppler.hip
 DopplerFn doppler_fn_f16(uint32_t nc, int mti, bool fast);            // inst_doppler_h16.hip
-// inst_doppler_s48.hip (nullptr: unsupported); pair = the S48 pair form (K1 tiles of T = 2 chirps)
-DopplerFn doppler_fn_s48(uint32_t nc, int mti, bool fast, bool pair);
+// inst_doppler_s48.hip (nullptr: unsupported); form: the S48 form K1 wrote, by its tile width T
+enum S48Form { kS48Quad = 0, kS48Pair = 1, kS48Strided = 2 };
+inline int s48_form(int range_T) { return range_T == 2 ? kS48Pair : range_T == 4 ? kS48Strided : kS48Quad; }
+DopplerFn doppler_fn_s48(uint32_t nc, int mti, bool fast, int form);
 inline DopplerInfo doppler_info(uint32_t nc, int mti = FMCW_MTI_OFF, int spec = FMCW_SPEC_F32, bool fast = false,
                                 bool q15 = false, int range_T = 4) {
   DopplerFn fn = spec == FMCW_SPEC_F16   ? doppler_fn_f16(nc, mti, fast)
-                 : spec == FMCW_SPEC_S48 ? doppler_fn_s48(nc, mti, fast, range_T == 2)
+                 : spec == FMCW_SPEC_S48 ? doppler_fn_s48(nc, mti, fast, s48_form(range_T))
                                          : doppler_fn_f32(nc, mti, fast, q15);
   switch (nc) {
 #define D_(N) case N: return {fn, DopplerGeom<N>::WR, DopplerGeom<N>::NT};

@@ -15,7 +15,11 @@ RangeFn range_fn_t(int dtype, bool q15) {
 }
 template <int N>
 RangeFn range_fn(int dtype, bool q15, int spec) {
-  if constexpr (N <= 2048) {  // S48 above N = 2048: the pair kernels (range_sq / range_px)
+  // S48: the strided-quad form at T = 4 (N = 1024), else quad (T >= 8) / pair (N = 2048); above
+  // N = 2048 the pair kernels (range_sq / range_px)
+  if constexpr (RangeGeom<N>::T == 4) {
+    if (spec == FMCW_SPEC_S48) return q15 ? nullptr : range_fn_t<N, SP_S48S>(dtype, false);
+  } else if constexpr (N <= 2048) {
     if (spec == FMCW_SPEC_S48) return q15 ? nullptr : range_fn_t<N, SP_S48>(dtype, false);
   }
   return spec == FMCW_SPEC_F16 ? range_fn_t<N, SP_F16>(dtype, q15) : spec == FMCW_SPEC_F32 ? range_fn_t<N, SP_F32>(dtype, q15)

@@ -120,14 +120,15 @@ struct LoadI16 {
 // holding X / N_range (|X| <= N max|x| would overflow fp16 for ADC-scale input; the 2^-log2 N
 // scale is exact and K2 undoes it at load).
 // Spectrum formats (fmcw.h fmcw_spectrum_dtype): SP_F32 float2 (8 B), SP_F16 half2 of X / N (4 B),
-// S48 (6 B, below) in its quad (SP_S48) or pair (SP_S48P) form.  K1 kernels take SP_S48 and pick
-// the form from their tile width T; K2 is instantiated per form.
-constexpr int SP_F32 = 0, SP_F16 = 1, SP_S48 = 2, SP_S48P = 3;
+// S48 (6 B, below) in its quad (SP_S48), pair (SP_S48P) or strided-quad (SP_S48S) form.  K1 kernels
+// take SP_S48 (quad or pair, from their tile width T) or SP_S48S; K2 is instantiated per form.
+constexpr int SP_F32 = 0, SP_F16 = 1, SP_S48 = 2, SP_S48P = 3, SP_S48S = 4;
 struct __attribute__((packed)) S48 { uint16_t h[3]; };  // one S48 point: pointer steps of 6 B
 template <int SP> struct SpecEl { using T = float2; };
 template <> struct SpecEl<SP_F16> { using T = uint32_t; };
 template <> struct SpecEl<SP_S48> { using T = S48; };
 template <> struct SpecEl<SP_S48P> { using T = S48; };
+template <> struct SpecEl<SP_S48S> { using T = S48; };
 typedef _Float16 fmcw_h2 __attribute__((ext_vector_type(2)));
 
 // ---- S48: the corner-turned spectrum in 6 bytes per point, one exponent per chirp group --------
@@ -177,6 +178,24 @@ __device__ __forceinline__ fmcw_u3v s48_pack(float2 v0, float2 v1, int q0) {
   w.y = ((i0 >> (32 - W - PB)) & 0xffffu) | (r1 << 16);                             // P0 32-47, P1 0-15
   w.z = ((r1 >> 16) & ((1u << (W - 16)) - 1)) | (b1 << (W - 16)) | (i1 << (W - 16 + PB));  // P1 16-47
   return w;
+}
+// Strided-quad form (SP_S48S): K2 lane t holds the 4 points of a quad (chirps t + 4 p k + p j,
+// j = 0..3, as K1 grouped them) in one 24-byte element, loaded as two 12-byte halves w0 (points 0,
+// 1) and w1 (points 2, 3): the exponent is assembled from the 4 records' 2-bit pieces in the lane,
+// no exchange; record j's bits 0-31 / 16-47 are byte-aligned slices of the 6 words.
+__device__ __forceinline__ void s48s_unpack4(fmcw_u3v w0, fmcw_u3v w1, float2 (&out)[4]) {
+  const uint32_t lo[4] = {w0.x, __builtin_amdgcn_alignbyte(w0.z, w0.y, 2), w1.x, __builtin_amdgcn_alignbyte(w1.z, w1.y, 2)};
+  const uint32_t hi[4] = {__builtin_amdgcn_alignbyte(w0.y, w0.x, 2), w0.z, __builtin_amdgcn_alignbyte(w1.y, w1.x, 2), w1.z};
+  uint32_t e = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) e |= __builtin_amdgcn_ubfe(lo[j], 23, 2) << (2 * j);
+  const float sc = __uint_as_float((e - 31) << 23);  // 2^(E - 31)
+  typedef float f2v __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f2v r = f2v{(float)(int)(lo[j] << 9), (float)(int)(hi[j] & 0xfffffe00u)} * f2v{sc, sc};
+    out[j] = make_float2(r.x, r.y);
+  }
 }
 // A 12-byte S48 store, padded: a VALU write of a wide store's data VGPRs within 2 wait states of
 // the store corrupts the stored data under load, and hipcc (ROCm 7.2, gfx950) pads that hazard
@@ -321,14 +340,22 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
   // order) wait for those stores too.  From N = 1024 a wave holds one chirp (P >= 64), so the
   // index is wave-uniform and the load goes through the scalar cache (lgkmcnt, not vmcnt).
   auto cw_index = [](int i) { return P >= 64 ? __builtin_amdgcn_readfirstlane(i) : i; };
+  // chirp q of group cb: cb T + q, or (SP_S48S, T = 4) the strided quad t + 4 p k + p q of K2's lane t
+  // (cb = t + p k, p = nc / 16 lanes per Doppler row), whose 4 points K2 then holds in one lane
+  static_assert(SP != SP_S48S || T == 4, "strided quads: 4 chirps per K1 group");
+  const int lgp = __builtin_ctz(nc) - 4;
+  auto chirp_of = [&](int cb) -> int {
+    if constexpr (SP == SP_S48S) return (cb & ((1 << lgp) - 1)) + ((cb >> lgp) << (lgp + 2)) + (q << lgp);
+    else return cb * T + q;
+  };
   float cw_n = 1.f;
   if (g < n_groups) {
     const int fr = g / ncb;
     const int cb = g - fr * ncb;
-    const size_t chirp = (size_t)fr * nc + (size_t)cb * T + q;
+    const size_t chirp = (size_t)fr * nc + (size_t)chirp_of(cb);
 #pragma unroll
     for (int m = 0; m < 8; ++m) a[m] = LD::fetch(cube, chirp * N + 2 * t0 + (N / 8) * m);
-    if (chirp_w) cw_n = chirp_w[cw_index(cb * T + q)];
+    if (chirp_w) cw_n = chirp_w[cw_index(chirp_of(cb))];
   }
   // window coefficients for samples 2t + {0,1} + (N/8) m, held for the whole kernel (round 4:
   // re-reading them every group below N = 4096 measured 845-848 k against 856-857 k frames/s)
@@ -393,10 +420,10 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
       if (gn < n_groups) {
         const int frn = gn / ncb;
         const int cbn = gn - frn * ncb;
-        const size_t chirp = (size_t)frn * nc + (size_t)cbn * T + q;
+        const size_t chirp = (size_t)frn * nc + (size_t)chirp_of(cbn);
 #pragma unroll
         for (int m = 0; m < 8; ++m) a[m] = LD::fetch(cube, chirp * N + 2 * t + (N / 8) * m);
-        if (chirp_w) cw_n = chirp_w[cw_index(cbn * T + q)];
+        if (chirp_w) cw_n = chirp_w[cw_index(chirp_of(cbn))];
       }
     }
     pass_sync<Gm::WG_SYNC>();
@@ -422,7 +449,7 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
         v1 = lds[(c0 + 1) * REG + pad16(r0 + i * (N / 8))];
       }
       if constexpr (SP == SP_F16) dst16[i * dstep / 2] = make_uint2(pack_h2(v0.x, v0.y), pack_h2(v1.x, v1.y));
-      else if constexpr (SP == SP_S48) {
+      else if constexpr (SP == SP_S48 || SP == SP_S48S) {
         store_b96_padded<kK1WriteThrough ? 16 /* sc1 */ : 0>(s48_pack<T >= 4 ? 4 : 2>(v0, v1, c0 & (T >= 4 ? 3 : 0)),
                                                             wrs, (uint32_t)((dbase + i * dstep) * sizeof(S48)), 0);
       }
@@ -1424,9 +1451,11 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
   using SE = typename SpecEl<SP>::T;
   const SE* const inter = reinterpret_cast<const SE*>(inter_in);
   const float sscale = SP == SP_F16 ? (float)ns : 1.f;  // undoes K1's 1 / N_range of an fp16 spectrum
+  constexpr bool S48S = SP == SP_S48S;  // strided quads: a lane's 4 points per element (no exchange)
   constexpr bool S48F = SP == SP_S48 || SP == SP_S48P;
   constexpr int SG = SP == SP_S48 ? 4 : 2;  // S48 exponent group: chirps per shared exponent
   static_assert(!S48F || (MTI == 0 && P % SG == 0), "S48: a lane group holds a chirp group");
+  static_assert(!S48S || MTI == 0, "S48: MTI off");
   // S48: this lane's chirps c = t + P m all sit at c % G = t % G of their group (t = lane % P);
   // the two lane constants are derived from t where they are used (not held across the loop)
   auto s48_sh = [](int tt) { return (uint32_t)(tt & 1) << 4; };   // byte offset x 8 of the record in its load
@@ -1491,7 +1520,8 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
            off_of((uint32_t)(ru >> lgRB) << lgncb, (uint32_t)(ru & ((1 << lgRB) - 1)), 0);
   };
   using PfT = std::conditional_t<SP == SP_S48P, fmcw_u3v, float2>;  // a prefetched point (raw for S48)
-  PfT nxt[PF ? NPF : 1];
+  PfT nxt[PF && !S48S ? NPF : 1];
+  fmcw_u3v nxq[PF && S48S ? NPF / 2 : 1];  // strided quads: two 12-B halves per prefetched quad
   const __amdgpu_buffer_rsrc_t srs = wt_rsrc(const_cast<SE*>(inter), 0xffffffffu);  // the prefetch's buffer loads
   // last-pass twiddle bases, once per lane (NC = 256: pass 1 + one radix-16 pass, k = t)
   constexpr bool TWH = NC / 16 <= 16 && P % 16 == 0;
@@ -1502,7 +1532,19 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
       if (tl < n_tiles) {
         const SE* p = unit_src(tl, rx);
         const int tq = opaque(t0);
-        if ((P & (T - 1)) == 0) {  // uniform: chirps t + P m sit a fixed S elements apart
+        if constexpr (S48S) {
+          // quad k of lane t: group cb = t + P k of the row block, element j = 0; groups P apart
+          const uint32_t vo = (uint32_t)((const char*)(p + (((uint32_t)tq << lgRB) << lgT)) - (const char*)inter);
+          const uint32_t sb = (((uint32_t)P << lgRB) << lgT) * (uint32_t)sizeof(S48);
+          uint32_t so = 0;
+#pragma unroll
+          for (int k = 0; k < NPF / 4; ++k) {
+            nxq[2 * k] = __builtin_bit_cast(fmcw_u3v, __builtin_amdgcn_raw_buffer_load_b96(srs, vo, so, 0));
+            nxq[2 * k + 1] = __builtin_bit_cast(fmcw_u3v, __builtin_amdgcn_raw_buffer_load_b96(srs, vo, so + 12u, 0));
+            so += sb;
+            asm volatile("" : "+s"(so));
+          }
+        } else if ((P & (T - 1)) == 0) {  // uniform: chirps t + P m sit a fixed S elements apart
           const SE* pb = p + ((((uint32_t)tq >> lgT) << lgRB) << lgT) + ((uint32_t)tq & (uint32_t)(T - 1));
           const uint32_t S = (uint32_t)(P >> lgT) << (lgRB + lgT);
           // the uniform m S byte offsets, one SGPR advanced per load: left to the compiler, the 16
@@ -1563,7 +1605,7 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
   // (measured: config 5 K2 177 -> 110 us per 4 frames; configs 2 / 3, whose workgroups read
   // whole lines, 2-3 % slower with it)
   // (S48: its 6-B points, so config 3's 96-B reads take the XCD mapping too)
-  const bool xcd = ((WPB * WR * (S48F ? 6 : 8)) << lgT) < 128;
+  const bool xcd = ((WPB * WR * (S48F || S48S ? 6 : 8)) << lgT) < 128;
   const int bid = xcd ? xcd_block_id((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
   prefetch(bid * WPB + wv, 0);
 
@@ -1587,7 +1629,8 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
     for (int rx = 0; rx < nrx; ++rx) {
       const SE* src = inter + ((size_t)f * nrx + rx) * (size_t)ns * NC;
       auto at = [&](uint32_t c) -> float2 {
-        if constexpr (SP == SP_S48P) return s48p_unpack(ld_s48_pair(src + off_of(rbase, rin, c), c & 1u), (uint32_t)t & 1u);
+        if constexpr (S48S) return make_float2(0.f, 0.f);  // (unused: the points come from vq)
+        else if constexpr (SP == SP_S48P) return s48p_unpack(ld_s48_pair(src + off_of(rbase, rin, c), c & 1u), (uint32_t)t & 1u);
         else if constexpr (S48F) return s48_unpack<SG>(ld_s48_raw<kNtSpecLd>(src + off_of(rbase, rin, c), c & 1u), (uint32_t)t & 1u, s48_qs(t));
         else return ld_spec<kNtSpecLd>(src + off_of(rbase, rin, c), sscale);
       };
@@ -1599,6 +1642,27 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
       // loads stay: with buffer loads the kernel needs 171 VGPRs, and held to 155 (3 waves) by
       // loading 8 points at a time it waits 3x longer on them (SQ_WAIT_INST_ANY per frame 15.4 M vs
       // fp32 5.3 M) and took 118 against 99-107 us per launch (profiles/r05/s48_pair/).
+      // strided quads: all 16 points decoded here, 4 per element, prefetched or loaded now
+      float2 vq[S48S ? 16 : 1];
+      if constexpr (S48S) {
+        const uint32_t q_vo = (uint32_t)((const char*)(src + off_of(rbase, rin, (uint32_t)t << lgT)) - (const char*)inter);
+        const uint32_t q_sb = (((uint32_t)P << lgRB) << lgT) * (uint32_t)sizeof(S48);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          fmcw_u3v w0, w1;
+          if (4 * k < NPF) {
+            w0 = nxq[4 * k < NPF ? 2 * k : 0];
+            w1 = nxq[4 * k < NPF ? 2 * k + 1 : 0];
+          } else {
+            w0 = __builtin_bit_cast(fmcw_u3v, __builtin_amdgcn_raw_buffer_load_b96(srs, q_vo, (uint32_t)k * q_sb, 0));
+            w1 = __builtin_bit_cast(fmcw_u3v, __builtin_amdgcn_raw_buffer_load_b96(srs, q_vo, (uint32_t)k * q_sb + 12u, 0));
+          }
+          float2 o[4];
+          s48s_unpack4(w0, w1, o);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) vq[4 * k + j] = o[j];
+        }
+      }
       uint32_t p_vo = 0, p_sb = 0;
       constexpr bool PBUF = SP == SP_S48P && NPF > 0;
       if constexpr (PBUF) {
@@ -1610,14 +1674,16 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
       for (int m = 0; m < 16; ++m) {
         const int c = t + P * m;
         float2 x;
-        if (PBUF && m >= NPF) {
+        if (S48S) {
+          x = vq[S48S ? m : 0];
+        } else if (PBUF && m >= NPF) {
           x = s48p_unpack(__builtin_bit_cast(fmcw_u3v, __builtin_amdgcn_raw_buffer_load_b96(srs, p_vo, (uint32_t)m * p_sb, 0)),
                           (uint32_t)t & 1u);
         } else if (m < NPF) {
           if constexpr (SP == SP_S48P) {
             x = s48p_unpack(nxt[m < NPF ? m : 0], (uint32_t)t & 1u);
           } else {
-            x = nxt[m < NPF ? m : 0];
+            x = nxt[m < NPF && !S48S ? m : 0];
             if constexpr (S48F) x = s48_unpack<SG>(fmcw_u2v{__float_as_uint(x.x), __float_as_uint(x.y)}, (uint32_t)t & 1u, s48_qs(t));
           }
         } else {

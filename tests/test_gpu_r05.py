@@ -28,21 +28,26 @@ from test_gpu_parity import check_map
 pytestmark = pytest.mark.gpu
 
 
-def test_headline_shape_parity(gpu):
+@pytest.mark.parametrize("spectrum", ["s48", "f32"])
+def test_headline_shape_parity(gpu, spectrum):
+    """(s48 is the bench's config-2 spectrum since round 5; f32 the fp32 path.)"""
     import sys
     if str(REPO) not in sys.path:
         sys.path.insert(0, str(REPO))
     import bench
     w = bench.WORKLOADS["c2"]
     F, ns, nc, nrx = w["frames"], w["ns"], w["nc"], w["nrx"]
-    assert (F, ns, nc, nrx, w["dtype"], w["cfar"]) == (1024, 1024, 256, 1, "f32", "os1d")
+    assert (F, ns, nc, nrx, w["dtype"], w["cfar"], w["spectrum"]) == (1024, 1024, 256, 1, "f32", "os1d", "s48")
     # bench.run_workload at rank 0: 16 distinct frames (seed 1234), tiled to F, resident in HBM
     n_u = 16
     u = np.ascontiguousarray(synth.frames(n_u, ns, nc, nrx, w["recipe"], seed=1234, dtype="f32"))
     fb = u.nbytes // n_u
-    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, N_RX=nrx, in_dtype="f32", cfar="os1d", max_frames=F) as core:
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, N_RX=nrx, in_dtype="f32", cfar="os1d", max_frames=F,
+                   spectrum=spectrum) as core:
         chunk = core.info("chunk")
-        assert chunk == 104 and F % chunk == 88      # ten chunks, the last one 88 frames
+        # f32: ten chunks of 104 frames, the last 88; s48 (6 B per point, same 208 MiB budget):
+        # seven of 138, the last 58
+        assert (chunk, F % chunk) == ((104, 88) if spectrum == "f32" else (138, 58))
         src = DeviceBuffer(u.nbytes)
         src.upload(u)
         cube = DeviceBuffer(F * fb)
@@ -60,7 +65,7 @@ def test_headline_shape_parity(gpu):
         dets = dd.download(DET_DTYPE, (n,))
         del cube, dd
         rd_map = rd.download(np.float32, (F, ns, nc))
-    # maps: frames 0, 624 (first of chunk 6) and 1023 vs the fp64 oracle of the frame they repeat
+    # maps: frames 0, 6 x chunk (first of chunk 6) and 1023 vs the fp64 oracle of the frame they repeat
     for f in (0, 6 * chunk, F - 1):
         ref = O.process(u[f % n_u].astype(np.complex128), None)["mag"]
         check_map(rd_map[f:f + 1], ref[None])

@@ -16,7 +16,7 @@ gfx950 correction: FETCH_SIZE reports half the bytes of a wide coalesced streami
 is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.  Units of both: KiB.
 
 usage: python tools/pmc_summary.py --fetch F.csv --write W.csv [--sq SQ.csv]
-       --frames c2=5120 --frames c3=80 --frames c5=80 --out profiles/pmc_r05.json
+       --frames c2=5120 --frames c3=80 --frames c5=80 [--spectrum c2=s48] --out profiles/pmc_r05.json
 """
 import argparse
 import collections
@@ -63,13 +63,21 @@ def main():
     ap.add_argument("--frames", action="append", default=[], help="workload=frames processed in the run")
     ap.add_argument("--command", default="python3 bench.py --steps 2 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-h2d")
     ap.add_argument("--out", default="profiles/pmc_r05.json")
+    ap.add_argument("--spectrum", action="append", default=[],
+                    help="workload=f32|s48: the spectrum format the run used (algorithmic bytes; default f32)")
     a = ap.parse_args()
     frames = {k: int(v) for k, v in (x.split("=") for x in a.frames)}
+    spec = dict(x.split("=") for x in a.spectrum)
+    for w, fmt in spec.items():  # K1 writes and K2 reads b_sp bytes per point instead of 8
+        b_sp = {"f32": 8, "f16": 4, "s48": 6}[fmt]
+        px = {"c2": 1024 * 256, "c3": 4096 * 512 * 4, "c5": 8192 * 1024}[w]
+        ALG[w]["k_range"] += px * (b_sp - 8)
+        ALG[w]["k_doppler"] += px * (b_sp - 8)
     tables = [read(a.fetch), read(a.write)] + ([read(a.sq)] if a.sq else [])
     out = {"method": "rocprofv3 --pmc FETCH_SIZE, --pmc WRITE_SIZE and --pmc SQ_* in separate runs of `"
                      + a.command + "`; per kernel: sum over its launches / frames it processed; "
                      "FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes",
-           "frames": frames, "workloads": {}}
+           "frames": frames, "spectrum": {w: spec.get(w, "f32") for w in frames}, "workloads": {}}
     # several kernel names may map to one (workload, kernel) entry (K3's three launches): the counters
     # are summed over all of them
     tot = collections.defaultdict(float)
@@ -101,7 +109,7 @@ def main():
                 if e["algorithmic_bytes_per_frame"]:
                     e["traffic_over_algorithmic"] = round(e["hbm_bytes_per_frame"] / e["algorithmic_bytes_per_frame"], 4)
             for key in list(e):
-                if isinstance(e[key], float):
+                if isinstance(e[key], float) and key != "traffic_over_algorithmic":
                     e[key] = round(e[key], 1)
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)
