@@ -159,17 +159,19 @@ __device__ __forceinline__ fmcw_u3v s48_pack(float2 v0, float2 v1, int q0) {
   constexpr uint32_t AB = 0x7fffffffu;
   const uint32_t mb = max(max(__float_as_uint(v0.x) & AB, __float_as_uint(v0.y) & AB),
                           max(__float_as_uint(v1.x) & AB, __float_as_uint(v1.y) & AB));
-  int el = __builtin_amdgcn_frexp_expf(__uint_as_float(mb));  // max < 2^el (0 for 0)
+  // E from the largest |component| m raised by 2^-(W-1) relative: m (1 + 2^-(W-1)) < 2^E gives
+  // m < 2^E (1 - 2^-W), so rint(|x| 2^(W-1-E)) <= 2^(W-1) - 1 and no significand needs a clamp (a
+  // group within 2^-W of a power of two takes the next exponent: one bit less, still within 2^-W)
+  int el = __builtin_amdgcn_frexp_expf(__uint_as_float(mb) * (1.0f + 1.0f / (1 << (W - 1))));
   if constexpr (G == 4) el = max(el, __builtin_amdgcn_mov_dpp(el, 0xB1 /* quad_perm [1,0,3,2]: lane ^ 1 */, 0xf, 0xf, false));
   const int E = max(el, -95);  // K2's scale 2^(E - 31) stays a normal float
   const uint32_t e8 = (uint32_t)(E + 127);
-  const int sh = W - 1 - E;
-  // |x| < 2^E, so -2^(W-1) <= q <= 2^(W-1): only the top can leave the W-bit range (clamped)
-  auto sig = [sh](float x) -> uint32_t {
-    const int q = (int)__builtin_rintf(__builtin_amdgcn_ldexpf(x, sh));
-    return (uint32_t)min(q, (1 << (W - 1)) - 1);
-  };
-  const uint32_t r0 = sig(v0.x), i0 = sig(v0.y), r1 = sig(v1.x), i1 = sig(v1.y);
+  // 2^(W-1-E) as a float (W-1-E in [-8, 117]: normal): one packed multiply scales re and im
+  const float sc = __uint_as_float((uint32_t)(W - 1 - E + 127) << 23);
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  const f2v s0 = f2v{v0.x, v0.y} * f2v{sc, sc}, s1 = f2v{v1.x, v1.y} * f2v{sc, sc};
+  auto sig = [](float x) -> uint32_t { return (uint32_t)(int)__builtin_rintf(x); };
+  const uint32_t r0 = sig(s0.x), i0 = sig(s0.y), r1 = sig(s1.x), i1 = sig(s1.y);
   constexpr uint32_t PM = (1u << PB) - 1;
   const uint32_t b0 = (e8 >> (PB * q0)) & PM, b1 = (e8 >> (PB * q0 + PB)) & PM;
   constexpr uint32_t MW = (1u << W) - 1;
