@@ -162,7 +162,8 @@ typedef struct fmcw_config {
  * Not with FMCW_COMPAT_MTI (its 16-bit words are defined on the fp32 spectrum).
  * FMCW_SPEC_S48 stores it in 6 bytes per point (config 2: 2 -> 1.5 MiB written and read back per
  * frame; configs 3 / 5: 64 -> 48 MiB, so the auto chunk holds 4 frames instead of 3): a group of
- * G chirps of a range bin shares one 8-bit exponent E (the largest of their 2G components is
+ * G chirps of a range bin (n_doppler / 16 apart at n_range = 1024, else adjacent) shares one 8-bit
+ * exponent E (the largest of their 2G components is
  * < 2^E), and every component is a W-bit signed significand of 2^(E - W + 1), i.e. exact to 2^-W
  * of the group's largest component (fp32: 2^-24 of each) -- G = 4, W = 23 at n_range <= 1024;
  * G = 2, W = 22 above.  The map stays within the 1e-4 tolerance of FMCW_SPEC_F32 (per frame and
