@@ -16,8 +16,8 @@ DopplerFn dfn_t(int mti, bool fast) {
 }
 template <int N>
 DopplerFn dfn(int mti, bool fast, int form) {
-  return form == kS48Pair ? dfn_t<N, SP_S48P>(mti, fast) : form == kS48Strided ? dfn_t<N, SP_S48S>(mti, fast)
-                                                                               : dfn_t<N, SP_S48>(mti, fast);
+  return form == kS48Pair ? dfn_t<N, SP_S48PS>(mti, fast) : form == kS48Strided ? dfn_t<N, SP_S48S>(mti, fast)
+                                                                                : dfn_t<N, SP_S48>(mti, fast);
 }
 }  // namespace
 

@@ -19,6 +19,8 @@ RangeFn range_fn(int dtype, bool q15, int spec) {
   // N = 2048 the pair kernels (range_sq / range_px)
   if constexpr (RangeGeom<N>::T == 4) {
     if (spec == FMCW_SPEC_S48) return q15 ? nullptr : range_fn_t<N, SP_S48S>(dtype, false);
+  } else if constexpr (RangeGeom<N>::T == 2 && N <= 2048) {
+    if (spec == FMCW_SPEC_S48) return q15 ? nullptr : range_fn_t<N, SP_S48PS>(dtype, false);
   } else if constexpr (N <= 2048) {
     if (spec == FMCW_SPEC_S48) return q15 ? nullptr : range_fn_t<N, SP_S48>(dtype, false);
   }
@@ -44,7 +46,7 @@ template <int N>
 RangeInfo range_sq(int dtype, int spec) {
   using S = SqPick<N>;
   constexpr int NT = N / S::V;
-  RangeFn fn = spec == FMCW_SPEC_S48 ? range_sq_t<N, SP_S48>(dtype) : range_sq_t<N, SP_F32>(dtype);
+  RangeFn fn = spec == FMCW_SPEC_S48 ? range_sq_t<N, SP_S48PS>(dtype) : range_sq_t<N, SP_F32>(dtype);
   return {fn, SqGeom<N, S::V>::T, SqGeom<N, S::V>::RB, NT, kRangeSeq};
 }
 
@@ -54,14 +56,14 @@ RangeInfo range_sq(int dtype, int spec) {
 template <int SP>
 RangeFn range_px_t(int dtype) {
   switch (dtype) {
-    case FMCW_IN_F32: return k_range_px<LoadF32, 4, SP == SP_S48 ? 6 : 4, SP>;
-    case FMCW_IN_F16: return k_range_px<LoadF16, 4, SP == SP_S48 ? 6 : 4, SP>;
-    case FMCW_IN_I16: return k_range_px<LoadI16, 4, SP == SP_S48 ? 6 : 4, SP>;
+    case FMCW_IN_F32: return k_range_px<LoadF32, 4, SP == SP_S48PS ? 6 : 4, SP>;
+    case FMCW_IN_F16: return k_range_px<LoadF16, 4, SP == SP_S48PS ? 6 : 4, SP>;
+    case FMCW_IN_I16: return k_range_px<LoadI16, 4, SP == SP_S48PS ? 6 : 4, SP>;
   }
   return nullptr;
 }
 RangeInfo range_px(int dtype, int spec) {
-  return {spec == FMCW_SPEC_S48 ? range_px_t<SP_S48>(dtype) : range_px_t<SP_F32>(dtype), 2, 64, 512, kRangePx};
+  return {spec == FMCW_SPEC_S48 ? range_px_t<SP_S48PS>(dtype) : range_px_t<SP_F32>(dtype), 2, 64, 512, kRangePx};
 }
 
 }  // namespace

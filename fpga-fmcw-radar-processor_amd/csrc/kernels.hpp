@@ -120,15 +120,20 @@ struct LoadI16 {
 // holding X / N_range (|X| <= N max|x| would overflow fp16 for ADC-scale input; the 2^-log2 N
 // scale is exact and K2 undoes it at load).
 // Spectrum formats (fmcw.h fmcw_spectrum_dtype): SP_F32 float2 (8 B), SP_F16 half2 of X / N (4 B),
-// S48 (6 B, below) in its quad (SP_S48), pair (SP_S48P) or strided-quad (SP_S48S) form.  K1 kernels
-// take SP_S48 (quad or pair, from their tile width T) or SP_S48S; K2 is instantiated per form.
-constexpr int SP_F32 = 0, SP_F16 = 1, SP_S48 = 2, SP_S48P = 3, SP_S48S = 4;
+// S48 (6 B, below) in its quad (SP_S48, T >= 8), strided-quad (SP_S48S, T = 4) or strided-pair
+// (SP_S48PS, T = 2) form; K1 and K2 are instantiated per form.  (Value 3 was round 5's first pair
+// form -- adjacent chirps, each K2 lane loading the pair's element and decoding one point; the
+// strided pair replaced it: config 3 23.9-24.5 k -> 24.4-24.5 k frames/s.)
+constexpr int SP_F32 = 0, SP_F16 = 1, SP_S48 = 2, SP_S48S = 4, SP_S48PS = 5;
+// strided S48 forms: the chirps a K1 group holds (and shares an exponent over) are the ones a K2
+// lane holds, p = n_doppler / 16 apart (section 3 of DESIGN.md)
+template <int SP> constexpr int s48_strided_g() { return SP == SP_S48S ? 4 : SP == SP_S48PS ? 2 : 0; }
 struct __attribute__((packed)) S48 { uint16_t h[3]; };  // one S48 point: pointer steps of 6 B
 template <int SP> struct SpecEl { using T = float2; };
 template <> struct SpecEl<SP_F16> { using T = uint32_t; };
 template <> struct SpecEl<SP_S48> { using T = S48; };
-template <> struct SpecEl<SP_S48P> { using T = S48; };
 template <> struct SpecEl<SP_S48S> { using T = S48; };
+template <> struct SpecEl<SP_S48PS> { using T = S48; };
 typedef _Float16 fmcw_h2 __attribute__((ext_vector_type(2)));
 
 // ---- S48: the corner-turned spectrum in 6 bytes per point, one exponent per chirp group --------
@@ -136,14 +141,16 @@ typedef _Float16 fmcw_h2 __attribute__((ext_vector_type(2)));
 // E = max frexp exponent of their 2G components (|x| < 2^E), clamped to >= -95; each component is
 // stored as q = rint(x 2^(W - 1 - E)), a W-bit two's-complement significand (clamped to
 // 2^(W-1) - 1), so |x - q 2^(E - W + 1)| <= 2^(E - W): 2^-W of the group's largest component (or
-// of 2^-95), where fp32 keeps 2^-24 of each.  Two forms, by K1's tile width T:
-//   quad (T >= 4, n_range <= 1024): G = 4, W = 23, 2 exponent bits per point;
-//   pair (T = 2, n_range >= 2048):  G = 2, W = 22, 4 exponent bits per point.
+// of 2^-95), where fp32 keeps 2^-24 of each.  By K1's tile width T:
+//   quad (T >= 8, n_range <= 512): G = 4 adjacent chirps, W = 23, 2 exponent bits per point;
+//   strided quad (T = 4, n_range = 1024): G = 4 chirps p apart (p = n_doppler / 16), W = 23;
+//   strided pair (T = 2, n_range >= 2048): G = 2 chirps p apart, W = 22, 4 exponent bits per point.
 // Point record (48 bits, little-endian, point q of the group at bytes 6q .. 6q + 5): bits 0 .. W-1
 // re, then the 8/G bits (8/G) q .. of e8 = E + 127, then im in the top W bits.
-// K1 lanes hold chirp pairs (c0, c0 + 1), c0 even; in the quad form they exchange the pair maximum
-// with the lane of the other pair of their quad (lane ^ 1).  K2 lanes t .. t + G - 1 (P % G == 0)
-// hold the group's chirps and OR their exponent pieces together across it (DPP).  Measured on the
+// K1 lanes hold chirp pairs (c0, c0 + 1) of the group, c0 even; in the quad forms they exchange the
+// pair maximum with the lane of the other pair (lane ^ 1).  K2: adjacent quads sit in lanes
+// t .. t + 3 (P % 4 == 0), which OR their exponent pieces together (DPP); a strided group sits in
+// one lane (the points t + p m it transforms), decoded from its whole element.  Measured on the
 // CPU model (fp64 oracle, per-bin error on bins >= 1e-3 of the frame peak): quad <= 3.3e-5 over 48
 // config-2 frames, pair 3.7e-8 at config 5 and 2.5e-8 at config 3, against 1e-4 allowed; one
 // exponent per point with 20-bit significands reached 1.9e-4 at config 2.
@@ -199,6 +206,21 @@ __device__ __forceinline__ void s48s_unpack4(fmcw_u3v w0, fmcw_u3v w1, float2 (&
     out[j] = make_float2(r.x, r.y);
   }
 }
+// Strided-pair form (SP_S48PS): a lane's points 2k, 2k + 1 (chirps t + 2 p k + p j) in one 12-byte
+// element, both decoded in the lane
+__device__ __forceinline__ void s48ps_unpack2(fmcw_u3v w, float2 (&out)[2]) {
+  constexpr int W = 22;
+  const uint32_t lo[2] = {w.x, __builtin_amdgcn_alignbyte(w.z, w.y, 2)};
+  const uint32_t hi[2] = {__builtin_amdgcn_alignbyte(w.y, w.x, 2), w.z};
+  const uint32_t e = __builtin_amdgcn_ubfe(w.x, W, 4) | (__builtin_amdgcn_ubfe(w.z, W - 16, 4) << 4);
+  const float sc = __uint_as_float((e - 31) << 23);  // 2^(E - 31)
+  typedef float f2v __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const f2v r = f2v{(float)(int)(lo[j] << (32 - W)), (float)(int)(hi[j] & ~((1u << (32 - W)) - 1))} * f2v{sc, sc};
+    out[j] = make_float2(r.x, r.y);
+  }
+}
 // A 12-byte S48 store, padded: a VALU write of a wide store's data VGPRs within 2 wait states of
 // the store corrupts the stored data under load, and hipcc (ROCm 7.2, gfx950) pads that hazard
 // only for stores whose soffset is not an SGPR -- k_range_px's S48 tile stores (SGPR soffset) came
@@ -238,32 +260,6 @@ template <bool NT>
 __device__ __forceinline__ fmcw_u2v ld_s48_raw(const S48* p, uint32_t odd) {
   return ld_u2<NT>(reinterpret_cast<const char*>(p) - 2 * odd);
 }
-// Pair form: both lanes of a pair load the pair's whole 12-byte element (from its 4-aligned start,
-// byte 6 p - 6 (p & 1)) and decode their own point with both exponent nibbles at hand -- no lane
-// exchange, and every load starts on the element (the 8-byte record loads of the quad form start
-// mid-element for odd points).
-__device__ __forceinline__ fmcw_u3v ld_s48_pair(const S48* p, uint32_t odd) {
-  const uint32_t* q = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(p) - 6 * odd);
-  fmcw_u3v w;
-  w.x = q[0];
-  w.y = q[1];
-  w.z = q[2];
-  return w;
-}
-__device__ __forceinline__ float2 s48p_unpack(fmcw_u3v w, uint32_t odd) {
-  constexpr int W = 22;
-  const uint32_t lo = odd ? w.y : w.x, hi = odd ? w.z : w.y;  // the point's record: bytes 2 odd .. of {lo, hi}
-  const uint32_t so = odd * 0x02020202u;
-  const uint32_t w0 = __builtin_amdgcn_perm(hi, lo, 0x03020100u + so);  // record bits 0-31
-  const uint32_t w1 = __builtin_amdgcn_perm(hi, lo, 0x05040302u + so);  // record bits 16-47
-  const float re = (float)(int)(w0 << (32 - W)), im = (float)(int)(w1 & ~((1u << (32 - W)) - 1));
-  const uint32_t e = __builtin_amdgcn_ubfe(w.x, W, 4) | (__builtin_amdgcn_ubfe(w.z, W - 16, 4) << 4);
-  const float sc = __uint_as_float((e - 31) << 23);  // 2^(E - 31)
-  typedef float f2v __attribute__((ext_vector_type(2)));
-  const f2v r = f2v{re, im} * f2v{sc, sc};
-  return make_float2(r.x, r.y);
-}
-
 __device__ __forceinline__ uint32_t pack_h2(float x, float y) {
   return __builtin_bit_cast(uint32_t, fmcw_h2{(_Float16)x, (_Float16)y});
 }
@@ -342,12 +338,13 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
   // order) wait for those stores too.  From N = 1024 a wave holds one chirp (P >= 64), so the
   // index is wave-uniform and the load goes through the scalar cache (lgkmcnt, not vmcnt).
   auto cw_index = [](int i) { return P >= 64 ? __builtin_amdgcn_readfirstlane(i) : i; };
-  // chirp q of group cb: cb T + q, or (SP_S48S, T = 4) the strided quad t + 4 p k + p q of K2's lane t
-  // (cb = t + p k, p = nc / 16 lanes per Doppler row), whose 4 points K2 then holds in one lane
-  static_assert(SP != SP_S48S || T == 4, "strided quads: 4 chirps per K1 group");
+  // chirp q of group cb: cb T + q, or (strided S48, T = G) t + T p k + p q, the chirps of K2's lane t
+  // (cb = t + p k, p = nc / 16 lanes per Doppler row), whose T points K2 then holds in one lane
+  constexpr int SGS = s48_strided_g<SP>();
+  static_assert(SGS == 0 || SGS == T, "strided S48: one exponent group per K1 group");
   const int lgp = __builtin_ctz(nc) - 4;
   auto chirp_of = [&](int cb) -> int {
-    if constexpr (SP == SP_S48S) return (cb & ((1 << lgp) - 1)) + ((cb >> lgp) << (lgp + 2)) + (q << lgp);
+    if constexpr (SGS > 0) return (cb & ((1 << lgp) - 1)) + ((cb >> lgp) << (lgp + __builtin_ctz(T))) + (q << lgp);
     else return cb * T + q;
   };
   float cw_n = 1.f;
@@ -451,7 +448,7 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
         v1 = lds[(c0 + 1) * REG + pad16(r0 + i * (N / 8))];
       }
       if constexpr (SP == SP_F16) dst16[i * dstep / 2] = make_uint2(pack_h2(v0.x, v0.y), pack_h2(v1.x, v1.y));
-      else if constexpr (SP == SP_S48 || SP == SP_S48S) {
+      else if constexpr (SP == SP_S48 || SGS > 0) {
         store_b96_padded<kK1WriteThrough ? 16 /* sc1 */ : 0>(s48_pack<T >= 4 ? 4 : 2>(v0, v1, c0 & (T >= 4 ? 3 : 0)),
                                                             wrs, (uint32_t)((dbase + i * dstep) * sizeof(S48)), 0);
       }
@@ -509,17 +506,24 @@ k_range_sq(const void* __restrict__ cube, float2* __restrict__ inter, const floa
   using RawT = std::conditional_t<E == 2, typename LD::Raw, typename LD::Raw1>;
   RawT a[M];
   float cwn = 1.f;
+  // chirp q of group cb: cb T + q, or (SP_S48PS) the strided pair t + 2 p k + p q (k_range's chirp_of)
+  const int lgp = __builtin_ctz(nc) - 4;
+  auto chirp_of = [&](int cb, int q) -> int {
+    if constexpr (SP == SP_S48PS) return (cb & ((1 << lgp) - 1)) + ((cb >> lgp) << (lgp + 1)) + (q << lgp);
+    else return cb * T + q;
+  };
   auto fetch = [&](int g, int q) {
     const int fr = g / ncb;
     const int cb = g - fr * ncb;
-    const size_t chirp = (size_t)fr * nc + (size_t)cb * T + q;
+    const int c = chirp_of(cb, q);
+    const size_t chirp = (size_t)fr * nc + (size_t)c;
     const int t = opaque(t0);
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       if constexpr (E == 2) a[m] = LD::fetch(cube, chirp * N + 2 * t + S0 * m);
       else a[m] = LD::fetch1(cube, chirp * N + t + S0 * m);
     }
-    if (chirp_w) cwn = chirp_w[__builtin_amdgcn_readfirstlane(cb * T + q)];
+    if (chirp_w) cwn = chirp_w[__builtin_amdgcn_readfirstlane(c)];
   };
   // range window of this thread's first-pass samples, held (V floats)
   float wh[V];
@@ -583,16 +587,17 @@ k_range_sq(const void* __restrict__ cube, float2* __restrict__ inter, const floa
     const int t = opaque(t0);
     const size_t fbase = (size_t)fr * N * nc;
     constexpr bool WT = kK1WriteThrough && N <= 4096;
-    constexpr size_t EB = SP == SP_S48 ? sizeof(S48) : sizeof(float2);  // bytes per point
+    constexpr bool S48V = SP == SP_S48 || SP == SP_S48PS;  // (S48 names the point struct)
+    constexpr size_t EB = S48V ? sizeof(S48) : sizeof(float2);  // bytes per point
     const __amdgpu_buffer_rsrc_t srs =  // one frame's tiles < 4 GiB
-        SP == SP_S48 ? wt_rsrc(reinterpret_cast<char*>(inter) + fbase * EB, 0xffffffffu) : wt_rsrc(inter + fbase, 0xffffffffu);
+        S48V ? wt_rsrc(reinterpret_cast<char*>(inter) + fbase * EB, 0xffffffffu) : wt_rsrc(inter + fbase, 0xffffffffu);
 #pragma unroll
     for (int gg = 0; gg < GF; ++gg)
 #pragma unroll
       for (int m = 0; m < RF; ++m) {
         const int d = t + P * gg + LL * m;
         const size_t off = ((size_t)(d / RB) * ncb + cb) * (RB * T) + (size_t)(d % RB) * T;
-        if constexpr (SP == SP_S48) {
+        if constexpr (S48V) {
           store_b96_padded<WT ? 16 /* sc1 */ : 0>(s48_pack<2>(X[0][gg][m], X[1][gg][m], 0), srs, (uint32_t)(off * EB), 0);
         } else {
           const float4 x = make_float4(X[0][gg][m].x, X[0][gg][m].y, X[1][gg][m].x, X[1][gg][m].y);
@@ -659,10 +664,17 @@ k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const floa
   constexpr int NTL = kNtCube ? 2 : 0;  // non-temporal cube loads (read once)
   Raw1 a[16];
   float cwn = 1.f;
+  // chirp q of group cb: cb T + q, or (SP_S48PS) the strided pair t + 2 p k + p q (k_range's chirp_of)
+  const int lgp = __builtin_ctz(nc) - 4;
+  auto chirp_of = [&](int cb, int q) -> int {
+    if constexpr (SP == SP_S48PS) return (cb & ((1 << lgp) - 1)) + ((cb >> lgp) << (lgp + 1)) + (q << lgp);
+    else return cb * T + q;
+  };
   auto fetch = [&](int g, int q) {
     const int fr = g / ncb;
     const int cb = g - fr * ncb;
-    const size_t chirp = (size_t)fr * nc + (size_t)cb * T + q;
+    const int c = chirp_of(cb, q);
+    const size_t chirp = (size_t)fr * nc + (size_t)c;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<char*>(reinterpret_cast<const char*>(cube)) + chirp * N * SB, (short)0, N * SB, 0x00020000);
     const int vo = opaque(t0) * SB;
@@ -674,7 +686,7 @@ k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const floa
         a[m] = __builtin_bit_cast(Raw1, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, m * 512 * SB, NTL));
       }
     }
-    if (chirp_w) cwn = chirp_w[__builtin_amdgcn_readfirstlane(cb * T + q)];
+    if (chirp_w) cwn = chirp_w[__builtin_amdgcn_readfirstlane(c)];
   };
   float wh[16 - WS];  // range window of samples t + 512 m, held (m < 16 - WS; the rest in wlds)
 #pragma unroll
@@ -763,8 +775,9 @@ k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const floa
     // tile stores: lane holds X[d] of both chirps for d = p (register m + 8) and p + 4096 (m)
     // d / 64 = (w >> 1) + 4 m' + 64 s, d % 64 = (l & 31) + 32 (w & 1); tile (d / 64, cb) is 1 KiB
     // (SP_S48: the pair form, 12-B elements in 768-B tiles)
-    constexpr int EB = SP == SP_S48 ? 2 * (int)sizeof(S48) : 16;  // bytes per (chirp 0, chirp 1) element
-    void* const fbase = SP == SP_S48 ? static_cast<void*>(reinterpret_cast<char*>(inter) + (size_t)fr * N * nc * (EB / 2))
+    constexpr bool S48V = SP == SP_S48 || SP == SP_S48PS;  // (S48 names the point struct)
+    constexpr int EB = S48V ? 2 * (int)sizeof(S48) : 16;  // bytes per (chirp 0, chirp 1) element
+    void* const fbase = S48V ? static_cast<void*>(reinterpret_cast<char*>(inter) + (size_t)fr * N * nc * (EB / 2))
                                      : static_cast<void*>(inter + (size_t)fr * N * nc);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(fbase, (short)0, N * nc * (EB / 2), 0x00020000);
     const int t = opaque(t0);
@@ -775,7 +788,7 @@ k_range_px(const void* __restrict__ cube, float2* __restrict__ inter, const floa
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int r = s ? m : m + 8;
-        if constexpr (SP == SP_S48) {
+        if constexpr (S48V) {
           store_b96_padded<0 /* write-back */>(s48_pack<2>(X[0][r], X[1][r], 0), rs, (uint32_t)vo,
                                                (4 * m + 64 * s) * ncb * (64 * EB));
         } else {
@@ -1434,7 +1447,7 @@ constexpr int k2_waves() { return (FAST && MTI == 0 && NC == 256) ? 4 : 2; }
 // and the 1-D CFAR, when enabled, at the reference geometry (8 refs / 2 guards per side, need =
 // n_ref - rank <= 4, fp32 compare).  The generic kernel keeps those as uniform runtime branches,
 // whose other arms held registers and SGPRs (spills to VGPR lanes) across the tile loop.
-// SP: the spectrum format K1 wrote (SP_F32, SP_F16, SP_S48 quad form (T >= 4, P % 4 == 0), SP_S48P
+// SP: the spectrum format K1 wrote (SP_F32, SP_F16, SP_S48 quad form (T >= 8, P % 4 == 0), SP_S48S / SP_S48PS
 // pair form (T = 2, P % 2 == 0); S48 with MTI off).
 template <int NC, int MTI, int SP = SP_F32, bool FAST = false>
 __global__ void __launch_bounds__(DopplerGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(k2_waves<NC, MTI, FAST>())))
@@ -1453,9 +1466,10 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
   using SE = typename SpecEl<SP>::T;
   const SE* const inter = reinterpret_cast<const SE*>(inter_in);
   const float sscale = SP == SP_F16 ? (float)ns : 1.f;  // undoes K1's 1 / N_range of an fp16 spectrum
-  constexpr bool S48S = SP == SP_S48S;  // strided quads: a lane's 4 points per element (no exchange)
-  constexpr bool S48F = SP == SP_S48 || SP == SP_S48P;
-  constexpr int SG = SP == SP_S48 ? 4 : 2;  // S48 exponent group: chirps per shared exponent
+  constexpr int SGS = s48_strided_g<SP>();  // strided S48: a lane's SGS points per element (no exchange)
+  constexpr bool S48S = SGS > 0;
+  constexpr bool S48F = SP == SP_S48;  // adjacent quads: exponent pieces ORed over a lane quad
+  constexpr int SG = 4;
   static_assert(!S48F || (MTI == 0 && P % SG == 0), "S48: a lane group holds a chirp group");
   static_assert(!S48S || MTI == 0, "S48: MTI off");
   // S48: this lane's chirps c = t + P m all sit at c % G = t % G of their group (t = lane % P);
@@ -1521,9 +1535,8 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
     return inter + ((size_t)fu * nrx + rx) * (size_t)ns * NC +
            off_of((uint32_t)(ru >> lgRB) << lgncb, (uint32_t)(ru & ((1 << lgRB) - 1)), 0);
   };
-  using PfT = std::conditional_t<SP == SP_S48P, fmcw_u3v, float2>;  // a prefetched point (raw for S48)
-  PfT nxt[PF && !S48S ? NPF : 1];
-  fmcw_u3v nxq[PF && S48S ? NPF / 2 : 1];  // strided quads: two 12-B halves per prefetched quad
+  float2 nxt[PF && !S48S ? NPF : 1];  // prefetched points (S48 quads: the raw 8 bytes)
+  fmcw_u3v nxq[PF && S48S ? NPF / 2 : 1];  // strided S48: 12-B loads (a quad's halves, or a pair)
   const __amdgpu_buffer_rsrc_t srs = wt_rsrc(const_cast<SE*>(inter), 0xffffffffu);  // the prefetch's buffer loads
   // last-pass twiddle bases, once per lane (NC = 256: pass 1 + one radix-16 pass, k = t)
   constexpr bool TWH = NC / 16 <= 16 && P % 16 == 0;
@@ -1535,14 +1548,15 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
         const SE* p = unit_src(tl, rx);
         const int tq = opaque(t0);
         if constexpr (S48S) {
-          // quad k of lane t: group cb = t + P k of the row block, element j = 0; groups P apart
+          // group k of lane t: K1 group cb = t + P k of the row block, element j = 0; groups P apart
           const uint32_t vo = (uint32_t)((const char*)(p + (((uint32_t)tq << lgRB) << lgT)) - (const char*)inter);
           const uint32_t sb = (((uint32_t)P << lgRB) << lgT) * (uint32_t)sizeof(S48);
           uint32_t so = 0;
 #pragma unroll
-          for (int k = 0; k < NPF / 4; ++k) {
-            nxq[2 * k] = __builtin_bit_cast(fmcw_u3v, __builtin_amdgcn_raw_buffer_load_b96(srs, vo, so, 0));
-            nxq[2 * k + 1] = __builtin_bit_cast(fmcw_u3v, __builtin_amdgcn_raw_buffer_load_b96(srs, vo, so + 12u, 0));
+          for (int k = 0; k < NPF / SGS; ++k) {
+#pragma unroll
+            for (int h = 0; h < SGS / 2; ++h)
+              nxq[(SGS / 2) * k + h] = __builtin_bit_cast(fmcw_u3v, __builtin_amdgcn_raw_buffer_load_b96(srs, vo, so + 12u * h, 0));
             so += sb;
             asm volatile("" : "+s"(so));
           }
@@ -1556,13 +1570,7 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
           const uint32_t sb = S * (uint32_t)sizeof(SE);
 #pragma unroll
           for (int m = 0; m < NPF; ++m) {
-            if constexpr (SP == SP_S48P) {
-              // the point's whole pair element (decoded at use)
-              const uint32_t vo = (uint32_t)((const char*)pb - (const char*)inter) - 6u * ((uint32_t)tq & 1u);
-              nxt[m] = __builtin_bit_cast(fmcw_u3v, __builtin_amdgcn_raw_buffer_load_b96(srs, vo, so, kNtSpecLd ? 2 /* nt */ : 0));
-              so += sb;
-              asm volatile("" : "+s"(so));
-            } else if constexpr (S48F) {
+            if constexpr (S48F) {
               // the raw 8 bytes at the point's record rounded down to 4 (decoded at use)
               const uint32_t vo = (uint32_t)((const char*)pb - (const char*)inter) - (s48_sh(tq) >> 3);
               typedef float f2v __attribute__((ext_vector_type(2)));
@@ -1590,9 +1598,7 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
           for (int m = 0; m < NPF; ++m) {
             const uint32_t c = (uint32_t)(tq + P * m);
             const SE* pc = p + ((((c >> lgT) << lgRB) << lgT) | (c & (uint32_t)(T - 1)));
-            if constexpr (SP == SP_S48P) {
-              nxt[m] = ld_s48_pair(pc, (uint32_t)tq & 1u);
-            } else if constexpr (S48F) {
+            if constexpr (S48F) {
               const fmcw_u2v r = ld_s48_raw<kNtSpecLd>(pc, (uint32_t)tq & 1u);
               nxt[m] = make_float2(__uint_as_float(r.x), __uint_as_float(r.y));
             } else {
@@ -1632,62 +1638,45 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
       const SE* src = inter + ((size_t)f * nrx + rx) * (size_t)ns * NC;
       auto at = [&](uint32_t c) -> float2 {
         if constexpr (S48S) return make_float2(0.f, 0.f);  // (unused: the points come from vq)
-        else if constexpr (SP == SP_S48P) return s48p_unpack(ld_s48_pair(src + off_of(rbase, rin, c), c & 1u), (uint32_t)t & 1u);
         else if constexpr (S48F) return s48_unpack<SG>(ld_s48_raw<kNtSpecLd>(src + off_of(rbase, rin, c), c & 1u), (uint32_t)t & 1u, s48_qs(t));
         else return ld_spec<kNtSpecLd>(src + off_of(rbase, rin, c), sscale);
       };
       float2 v[16];
-      // S48 pair form with a prefetch (NC = 512): the points not prefetched by buffer loads of the
-      // whole pair element, the lane's byte offset in a VGPR and the uniform m S part in the SGPR
-      // offset -- flat 64-bit addresses per point took 183 VGPRs (2 waves per SIMD) against fp32's
-      // 165 (3): config-3 K2 82 -> 60 us per 4-frame launch.  At NC = 1024 (no prefetch) the flat
-      // loads stay: with buffer loads the kernel needs 171 VGPRs, and held to 155 (3 waves) by
-      // loading 8 points at a time it waits 3x longer on them (SQ_WAIT_INST_ANY per frame 15.4 M vs
-      // fp32 5.3 M) and took 118 against 99-107 us per launch (profiles/r05/s48_pair/).
-      // strided quads: all 16 points decoded here, 4 per element, prefetched or loaded now
+      // strided S48: all 16 points decoded here, SGS per element, prefetched or loaded now
       float2 vq[S48S ? 16 : 1];
       if constexpr (S48S) {
         const uint32_t q_vo = (uint32_t)((const char*)(src + off_of(rbase, rin, (uint32_t)t << lgT)) - (const char*)inter);
         const uint32_t q_sb = (((uint32_t)P << lgRB) << lgT) * (uint32_t)sizeof(S48);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          fmcw_u3v w0, w1;
-          if (4 * k < NPF) {
-            w0 = nxq[4 * k < NPF ? 2 * k : 0];
-            w1 = nxq[4 * k < NPF ? 2 * k + 1 : 0];
-          } else {
-            w0 = __builtin_bit_cast(fmcw_u3v, __builtin_amdgcn_raw_buffer_load_b96(srs, q_vo, (uint32_t)k * q_sb, 0));
-            w1 = __builtin_bit_cast(fmcw_u3v, __builtin_amdgcn_raw_buffer_load_b96(srs, q_vo, (uint32_t)k * q_sb + 12u, 0));
-          }
-          float2 o[4];
-          s48s_unpack4(w0, w1, o);
+        for (int k = 0; k < 16 / SGS; ++k) {
+          fmcw_u3v w[SGS / 2];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) vq[4 * k + j] = o[j];
+          for (int h = 0; h < SGS / 2; ++h) {
+            if (SGS * k < NPF) w[h] = nxq[SGS * k < NPF ? (SGS / 2) * k + h : 0];
+            else w[h] = __builtin_bit_cast(fmcw_u3v, __builtin_amdgcn_raw_buffer_load_b96(srs, q_vo, (uint32_t)k * q_sb + 12u * h, 0));
+          }
+          if constexpr (SGS == 4) {
+            float2 o[4];
+            s48s_unpack4(w[0], w[SGS / 2 - 1], o);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) vq[4 * k + j] = o[j];
+          } else {
+            float2 o[2];
+            s48ps_unpack2(w[0], o);
+            vq[2 * k] = o[0];
+            vq[2 * k + 1] = o[1];
+          }
         }
       }
-      uint32_t p_vo = 0, p_sb = 0;
-      constexpr bool PBUF = SP == SP_S48P && NPF > 0;
-      if constexpr (PBUF) {
-        p_vo = (uint32_t)((const char*)(src + off_of(rbase, rin, (uint32_t)t)) - (const char*)inter) - 6u * ((uint32_t)t & 1u);
-        p_sb = ((uint32_t)(P >> lgT) << (lgRB + lgT)) * (uint32_t)sizeof(S48);
-      }
-      static_assert(!PBUF || P % 2 == 0, "pair form: chirps t + P m sit m S elements apart");
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int c = t + P * m;
         float2 x;
         if (S48S) {
           x = vq[S48S ? m : 0];
-        } else if (PBUF && m >= NPF) {
-          x = s48p_unpack(__builtin_bit_cast(fmcw_u3v, __builtin_amdgcn_raw_buffer_load_b96(srs, p_vo, (uint32_t)m * p_sb, 0)),
-                          (uint32_t)t & 1u);
         } else if (m < NPF) {
-          if constexpr (SP == SP_S48P) {
-            x = s48p_unpack(nxt[m < NPF ? m : 0], (uint32_t)t & 1u);
-          } else {
-            x = nxt[m < NPF && !S48S ? m : 0];
-            if constexpr (S48F) x = s48_unpack<SG>(fmcw_u2v{__float_as_uint(x.x), __float_as_uint(x.y)}, (uint32_t)t & 1u, s48_qs(t));
-          }
+          x = nxt[m < NPF && !S48S ? m : 0];
+          if constexpr (S48F) x = s48_unpack<SG>(fmcw_u2v{__float_as_uint(x.x), __float_as_uint(x.y)}, (uint32_t)t & 1u, s48_qs(t));
         } else {
           x = at((uint32_t)c);
         }
