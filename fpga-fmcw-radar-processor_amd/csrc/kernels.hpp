@@ -227,6 +227,8 @@ __device__ __forceinline__ void s48ps_unpack2(fmcw_u3v w, float2 (&out)[2]) {
 // out with the next element's packing writing into the previous store's data VGPRs at once, and
 // the first frame of multi-group launches read back wrong under load (tools/store_hazard_scan.py
 // finds such sequences in a .s).  The two wait states are placed here, fenced against scheduling.
+// (k_range / k_range_sq store with soffset 0, which hipcc pads itself: they use the plain store,
+// config-2 K1 74.3-74.7 against 74.6-75.2 us per launch with the fenced one.)
 template <int AUX>
 __device__ __forceinline__ void store_b96_padded(fmcw_u3v w, __amdgpu_buffer_rsrc_t rs, uint32_t vo, uint32_t so) {
   __builtin_amdgcn_raw_buffer_store_b96(w, rs, vo, so, AUX);
@@ -449,8 +451,10 @@ k_range(const void* __restrict__ cube, float2* __restrict__ inter, const float* 
       }
       if constexpr (SP == SP_F16) dst16[i * dstep / 2] = make_uint2(pack_h2(v0.x, v0.y), pack_h2(v1.x, v1.y));
       else if constexpr (SP == SP_S48 || SGS > 0) {
-        store_b96_padded<kK1WriteThrough ? 16 /* sc1 */ : 0>(s48_pack<T >= 4 ? 4 : 2>(v0, v1, c0 & (T >= 4 ? 3 : 0)),
-                                                            wrs, (uint32_t)((dbase + i * dstep) * sizeof(S48)), 0);
+        // (soffset 0: hipcc pads the store-data hazard itself here, see store_b96_padded)
+        __builtin_amdgcn_raw_buffer_store_b96(s48_pack<T >= 4 ? 4 : 2>(v0, v1, c0 & (T >= 4 ? 3 : 0)), wrs,
+                                              (uint32_t)((dbase + i * dstep) * sizeof(S48)), 0,
+                                              kK1WriteThrough ? 16 /* sc1 */ : 0);
       }
       else if constexpr (kK1WriteThrough && N <= 4096) st_f4_wt(wrs, (uint32_t)((dbase + i * dstep) * sizeof(float2)), make_float4(v0.x, v0.y, v1.x, v1.y));
       else st_f4<kNtSpecSt>(dst + i * dstep, make_float4(v0.x, v0.y, v1.x, v1.y));
@@ -598,7 +602,8 @@ k_range_sq(const void* __restrict__ cube, float2* __restrict__ inter, const floa
         const int d = t + P * gg + LL * m;
         const size_t off = ((size_t)(d / RB) * ncb + cb) * (RB * T) + (size_t)(d % RB) * T;
         if constexpr (S48V) {
-          store_b96_padded<WT ? 16 /* sc1 */ : 0>(s48_pack<2>(X[0][gg][m], X[1][gg][m], 0), srs, (uint32_t)(off * EB), 0);
+          __builtin_amdgcn_raw_buffer_store_b96(s48_pack<2>(X[0][gg][m], X[1][gg][m], 0), srs, (uint32_t)(off * EB), 0,
+                                                WT ? 16 /* sc1 */ : 0);  // (soffset 0: padded by hipcc)
         } else {
           const float4 x = make_float4(X[0][gg][m].x, X[0][gg][m].y, X[1][gg][m].x, X[1][gg][m].y);
           if constexpr (WT) st_f4_wt(srs, (uint32_t)(off * sizeof(float2)), x);
