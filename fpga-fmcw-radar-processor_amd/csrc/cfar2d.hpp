@@ -788,25 +788,38 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
 // (tools/k3_screen_model.py --rules): survivors 1.60 % -> 0.033 % (config 5), 0.014 % -> 0.009 %
 // (config 3).
 //
-// LDS per ring row: two nibble-seed rows (bit 0 / bit 4 of a byte: key16 >= QA / QB, and >= QC /
-// QD) with circular halos, and a cut-code row (a nibble per cell: key16 < UA, UB, U2A, U2B) --
-// 2.5 B per cell instead of round 4's 3 B (key16 + one seed row), so config 5 fits 4 workgroups per
-// CU (39.3 KB each).  Every rule is exact in its own right; a cell that passes none of them goes to
-// K3b (key16(cut) is an upper bound: the rules only ever keep more cells).
+// LDS per ring row: two nibble PREFIX rows and a cut-code row (a nibble per cell: key16 < UA, UB, U2A,
+// U2B).  A prefix row holds per cell one byte of two 4-bit counters: nibble 0 = #{rows y of the strip
+// so far, in its walk order, with key16 >= QA} mod 16, nibble 1 the same for QB (second row: QC / QD),
+// with circular halos.  A window's column count (<= 2 HR + 1 = 11 < 16) is then the nibble-wise
+// difference of two rows mod 16 (round 5; before: the sum of the 11 rows' level bits, 44 LDS reads
+// and 194 adds per lane and step, now 12 reads and 22 nibble differences), at 2.5 B per cell; the
+// ring holds one row more (TR + 2 HR + 1) for the difference.  Every rule is exact in its own right; a
+// cell that passes none of them goes to K3b (key16(cut) is an upper bound: the rules only ever keep
+// more cells).
 template <int NC, int HR, int GR> struct LvGeom {
   static constexpr int NT = 256, WPB = 4, WR = DopplerGeom<NC>::WR, TR = WPB * WR, TPR = NC / 16;
-  static constexpr int RB = NC + 2 * MH + 16;   // seed row stride (bytes; b7idx layout, circular halos)
+  static constexpr int RB = NC + 16;            // prefix row (bytes): cell d (-8 <= d < NC + 8) at byte d + 8
   static constexpr int CS = NC / 2;             // cut-code row (a nibble per cell, no halos)
-  static constexpr int NR = TR + 2 * HR;        // ring rows
+  static constexpr int ROWB = 2 * RB + CS;      // one ring slot: A / B prefixes, C / D prefixes, cut codes
+  static constexpr int NR = TR + 2 * HR + 1;    // ring rows
   static constexpr int N_REF = (2 * HR + 1) * 13 - (2 * GR + 1) * 5;
   static constexpr int HIST = 128 + 16;         // u32: level histogram + counters
-  static constexpr int CAPB = 256, CAPT = 128;  // strip buffer: survivor cells, (tile, run) pairs
-  static constexpr size_t SMEM = (size_t)NR * (2 * RB + CS) + (HIST + CAPB + 2 * CAPT) * 4;
-  static_assert(RB % 16 == 0 && CS % 8 == 0 && TR * NC == 16 * NT, "a step's rows are 16 cells per thread");
+  static constexpr int CAPB = 192, CAPT = 64;   // strip buffer: survivor cells, (tile, run) pairs
+  static constexpr size_t SMEM = (size_t)NR * ROWB + (HIST + CAPB + 2 * CAPT) * 4;
+  static_assert(RB % 16 == 0 && ROWB % 16 == 0 && TR * NC == 16 * NT, "a step's rows are 16 cells per thread");
 };
+__host__ __device__ constexpr int pidx(int d) { return d + 8; }
 
 template <int NC, int HR, int GR>
 constexpr size_t cfar2d_lv_smem_bytes() { return LvGeom<NC, HR, GR>::SMEM; }
+
+// nibble-wise (p + w) mod 16 for w with nibbles 0 / 1
+__device__ __forceinline__ uint32_t nib_add(uint32_t p, uint32_t w) { return ((p & 0x77777777u) + w) ^ (p & 0x88888888u); }
+// nibble-wise (a - b) mod 16: (a | 8) - (b & 7) never borrows; bit 3 flips where a and b agree in it
+__device__ __forceinline__ uint32_t nib_sub(uint32_t a, uint32_t b) {
+  return ((a | 0x88888888u) - (b & 0x77777777u)) ^ (~(a ^ b) & 0x88888888u);
+}
 
 // The four cut-code flags of 4 cells (kw: their key16 pairs) as a 16-bit word of nibbles (cell j in
 // bits 4j .. 4j + 3; bit k = key16 < U_k, W_k = (U_k | 0x8000) - 1 in both halves, as
@@ -822,58 +835,38 @@ __device__ __forceinline__ uint32_t lv_cut_code(uint2 kw, const uint32_t (&W)[4]
   return (t & 0xffu) | ((t >> 8) & 0xff00u);
 }
 
-// Survivor bits (bit j: cell d0 + j may detect) of this lane's 16 CUTs, CUT row rl of the group tile.
-template <int NC, int HR, int GR>
-__device__ __forceinline__ uint32_t cfar2d_screen_rules(const uint8_t* ab, const uint8_t* cd, const uint8_t* code,
-                                                        int base, int rl, int d0, int need, bool ruleA) {
-  using Gm = LvGeom<NC, HR, GR>;
-  constexpr int NR = Gm::NR, RB = Gm::RB, CS = Gm::CS, NW = 2 * HR + 1;
-  static_assert(Gm::N_REF == 128 && 2 * HR + 1 <= 15 && 5 * (2 * GR + 1) <= 15, "thresholds below are for n_ref 128");
-  // column sums: V (seeds A/B) over the window rows, G over the guard rows, W (seeds C/D) over the box;
-  // a rolling window of kK3ScreenAhead rows of LDS reads in flight (sched_barrier + opaque sums)
+// Survivor bits (bit j: cell d0 + j may detect) of a lane's 16 CUTs from the prefix rows: hiA / loA
+// (A / B levels) and hiC / loC (C / D) the 32-byte windows (cells d0 - 8 .. d0 + 23) of the two rows
+// whose difference is the window's column counts, hiG / loG those of the guard rows, cw the CUTs' 16
+// code nibbles.
+template <int HR, int GR>
+__device__ __forceinline__ uint32_t cfar2d_screen_prefix(const uint8_t* hiA, const uint8_t* loA, const uint8_t* hiC,
+                                                         const uint8_t* loC, const uint8_t* hiG, const uint8_t* loG,
+                                                         uint2 cw, int need, bool ruleA) {
+  static_assert((2 * HR + 1) * 13 - (2 * GR + 1) * 5 == 128 && 2 * HR + 1 <= 15 && 5 * (2 * GR + 1) <= 15,
+                "thresholds below are for n_ref 128");
   uint32_t V[8], G[6], W[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) V[k] = W[k] = 0u;
-#pragma unroll
-  for (int k = 0; k < 6; ++k) G[k] = 0u;
-  constexpr int AH = kK3ScreenAhead < NW ? kK3ScreenAhead : NW;
-  int sl = rl + base;
-  sl = sl >= NR ? sl - NR : sl;
-  uint4 qa[AH], qb[AH], qc[AH], qd[AH];
-  auto load_row = [&](int j) {
-    const uint8_t* pa = ab + sl * RB + b7idx(d0 - 8);
-    const uint8_t* pc = cd + sl * RB + b7idx(d0 - 8);
-    qa[j % AH] = *reinterpret_cast<const uint4*>(pa);
-    qb[j % AH] = *reinterpret_cast<const uint4*>(pa + 16);
-    qc[j % AH] = *reinterpret_cast<const uint4*>(pc);
-    qd[j % AH] = *reinterpret_cast<const uint4*>(pc + 16);
-    sl = sl + 1 == NR ? 0 : sl + 1;
-  };
-#pragma unroll
-  for (int j = 0; j < AH; ++j) load_row(j);
-#pragma unroll
-  for (int j = 0; j < NW; ++j) {
-    const int dr = j - HR;
-    __builtin_amdgcn_sched_barrier(0);
-    const uint4 a0 = qa[j % AH], a1 = qb[j % AH], c0 = qc[j % AH], c1 = qd[j % AH];
-    const uint32_t D[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-    const uint32_t E[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-    if (j + AH < NW) load_row(j + AH);
+  {
+    const uint4 a0 = *reinterpret_cast<const uint4*>(hiA), a1 = *reinterpret_cast<const uint4*>(hiA + 16);
+    const uint4 b0 = *reinterpret_cast<const uint4*>(loA), b1 = *reinterpret_cast<const uint4*>(loA + 16);
+    const uint4 c0 = *reinterpret_cast<const uint4*>(hiC), c1 = *reinterpret_cast<const uint4*>(hiC + 16);
+    const uint4 e0 = *reinterpret_cast<const uint4*>(loC), e1 = *reinterpret_cast<const uint4*>(loC + 16);
+    const uint4 g0 = *reinterpret_cast<const uint4*>(hiG), g1 = *reinterpret_cast<const uint4*>(hiG + 16);
+    const uint4 h0 = *reinterpret_cast<const uint4*>(loG), h1 = *reinterpret_cast<const uint4*>(loG + 16);
+    const uint32_t A[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const uint32_t B[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    const uint32_t C[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    const uint32_t E[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+    const uint32_t Gh[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const uint32_t Gl[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      V[k] += D[k];
-      W[k] += E[k];
-    }
-    if (dr >= -GR && dr <= GR) {
-#pragma unroll
-      for (int k = 0; k < 6; ++k) G[k] += D[k + 1];
+      V[k] = nib_sub(A[k], B[k]);
+      W[k] = nib_sub(C[k], E[k]);
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(V[k]), "+v"(W[k]));
-#pragma unroll
-    for (int k = 0; k < 6; ++k) asm volatile("" : "+v"(G[k]));
+    for (int k = 0; k < 6; ++k) G[k] = nib_sub(Gh[k + 1], Gl[k + 1]);
   }
-  __builtin_amdgcn_sched_barrier(0);
   // 13-cell window sums per level (bytes: cell d0 + 4m + t in word m byte t)
   uint32_t HA[4], HB[4], HC[4], HD[4];
   {
@@ -895,7 +888,7 @@ __device__ __forceinline__ uint32_t cfar2d_screen_rules(const uint8_t* ab, const
     lv_sum13(XA, HC);
     lv_sum13(XB, HD);
   }
-  // guard block (3 x 5 around the CUT) of seeds A / B in the nibbles
+  // guard block (3 x 5 around the CUT) of levels A / B in the nibbles
   uint32_t H5[4];
   {
     uint32_t Gp[5], S2[5], S4[4];
@@ -908,10 +901,6 @@ __device__ __forceinline__ uint32_t cfar2d_screen_rules(const uint8_t* ab, const
 #pragma unroll
     for (int m = 0; m < 4; ++m) H5[m] = S4[m] + Gp[m + 1];
   }
-  // the 16 CUTs' code nibbles (cells d0 .. d0 + 15 of the CUT row)
-  int cs = rl + HR + base;
-  cs = cs >= NR ? cs - NR : cs;
-  const uint2 cw = *reinterpret_cast<const uint2*>(code + cs * CS + d0 / 2);
   constexpr uint32_t H = 0x80808080u;
   auto K = [](int v) { return (uint32_t)v * 0x01010101u; };
   const uint32_t k_need = K(128 - need);
@@ -935,19 +924,26 @@ __device__ __forceinline__ uint32_t cfar2d_screen_rules(const uint8_t* ab, const
   return bits;
 }
 
+// k_cfar2d_lv at NC = 1024: thread t stages cells 4t .. 4t + 3 of every ring row (NC / 4 = NT), so
+// it carries its column's two running prefixes from row to row in registers.  Ring tile row x is
+// map row r0 - HR - xo + x (xo = 1 walking downwards, 0 upwards: the extra row lies on the side the
+// prefix starts from); the strip's first step stages all NR rows in walk order, every later step
+// the TR new ones (prefetched a step ahead: buffer loads whose range check returns the zero rows
+// off the map).  For CUT row rl the window's column counts are P[rl + 2 HR + 1] - P[rl] (downwards;
+// upwards the prefix runs the other way and the difference flips), the guard rows'
+// P[rl + HR + GR + 1] - P[rl + HR - GR], the CUT row is tile row rl + HR + xo.
 template <int NC, int HR, int GR>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int frame0, int tile0, Cfar2DArgs a,
             DetSink sink, Cfar2Cands cands) {
   (void)frame0;
   using Gm = LvGeom<NC, HR, GR>;
-  constexpr int WR = Gm::WR, NT = Gm::NT, RB = Gm::RB, CS = Gm::CS, TPR = Gm::TPR, WPB = Gm::WPB, TR = Gm::TR;
+  static_assert(NC == 1024 && Gm::WR == 1 && NC / 4 == Gm::NT, "a thread stages one 4-cell column of every row");
+  constexpr int WR = Gm::WR, NT = Gm::NT, RB = Gm::RB, ROWB = Gm::ROWB, TPR = Gm::TPR, WPB = Gm::WPB, TR = Gm::TR;
   constexpr int NR = Gm::NR;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem8[];
-  uint8_t* const ab = smem8;
-  uint8_t* const cd = ab + NR * RB;
-  uint8_t* const code = cd + NR * RB;
-  uint32_t* const hist = reinterpret_cast<uint32_t*>(code + NR * CS);
+  uint8_t* const ring = smem8;
+  uint32_t* const hist = reinterpret_cast<uint32_t*>(ring + NR * ROWB);
   uint32_t* const cnt = hist + 128;    // [0..3] wave counts, [4] / [5] buffer fill, [6] / [7] flush bases
   uint32_t* const buf = cnt + 16;      // the strip's survivor cells (Gm::CAPB)
   uint32_t* const bt = buf + Gm::CAPB; // their wave tiles: (tile, offset << 16 | count) (Gm::CAPT)
@@ -984,66 +980,68 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
   const int wg_per_frame = (wt_per_frame + WPB - 1) / WPB;
   const int spf = (wg_per_frame + steps - 1) / steps;
   const int nf = n_strips / spf;
-  const int tid = opaque(threadIdx.x);
-  // a TR-row block of cells (4096) as 4 float4 per thread, lanes contiguous per load: float4 e4 =
-  // tid + u NT is row e4 / (NC / 4), cells 4 (e4 % (NC / 4)) .. + 3
-  auto blk = [](int u, int& i, int& d) {  // recomputed at each use (not held across the step)
-    const int e4 = opaque(threadIdx.x) + u * NT;
-    i = e4 / (NC / 4);
-    d = (e4 - i * (NC / 4)) * 4;
-  };
+  const int dt = 4 * (int)threadIdx.x;            // this thread's staged cells dt .. dt + 3
+  const bool halo_lo = dt < 8, halo_hi = dt >= NC - 8;
+  const int d0 = (lane % TPR) * 16;               // the lane's 16 CUTs (row wv of the step)
 
-  // per strip: level words (seed rows) and cut-code thresholds
+  // per strip: level words and cut-code thresholds (uniform)
   uint32_t qa2 = 0, qb2 = 0, qc2 = 0, qd2 = 0;
   uint32_t Wc[4] = {0, 0, 0, 0};
   bool ruleA = false;
-  auto put = [&](int x, int d, float4 v) {  // ring row x (0 = the step's first halo row), cells d .. d + 3
-    v = a.compat ? q17x4(v) : nonneg4(v);
-    const uint2 kw = make_uint2(key16(v.x) | (key16(v.y) << 16), key16(v.z) | (key16(v.w) << 16));
-    const uint32_t wab = lv_nibbles(kw, qa2, qb2), wcd = lv_nibbles(kw, qc2, qd2);
-    uint8_t* ra = ab + x * RB;
-    uint8_t* rc = cd + x * RB;
-    *reinterpret_cast<uint32_t*>(ra + b7idx(d)) = wab;
-    *reinterpret_cast<uint32_t*>(rc + b7idx(d)) = wcd;
-    if (d < MH) {
-      *reinterpret_cast<uint32_t*>(ra + b7idx(NC + d)) = wab;
-      *reinterpret_cast<uint32_t*>(rc + b7idx(NC + d)) = wcd;
+  uint32_t pab = 0, pcd = 0;  // this column's running prefixes (A / B, C / D)
+  // one ring slot's cells dt .. dt + 3: level bits into the prefixes, prefixes and cut codes to LDS
+  auto stage = [&](int slot, float4 v) {
+    if (a.compat) v = q17x4(v);
+    // key16 without the NaN / negative cells (-> 0): a sign or NaN bit pattern is above inf's
+    const uint32_t b0 = __float_as_uint(v.x), b1 = __float_as_uint(v.y), b2 = __float_as_uint(v.z),
+                   b3 = __float_as_uint(v.w);
+    const uint32_t s0 = b0 <= 0x7f800000u ? b0 : 0u, s1 = b1 <= 0x7f800000u ? b1 : 0u;
+    const uint32_t s2 = b2 <= 0x7f800000u ? b2 : 0u, s3 = b3 <= 0x7f800000u ? b3 : 0u;
+    const uint2 kw = make_uint2(__builtin_amdgcn_perm(s1, s0, 0x07060302u), __builtin_amdgcn_perm(s3, s2, 0x07060302u));
+    pab = nib_add(pab, lv_nibbles(kw, qa2, qb2));
+    pcd = nib_add(pcd, lv_nibbles(kw, qc2, qd2));
+    uint8_t* const rp = ring + slot * ROWB;
+    *reinterpret_cast<uint32_t*>(rp + pidx(dt)) = pab;
+    *reinterpret_cast<uint32_t*>(rp + RB + pidx(dt)) = pcd;
+    if (halo_lo) {
+      *reinterpret_cast<uint32_t*>(rp + pidx(dt + NC)) = pab;
+      *reinterpret_cast<uint32_t*>(rp + RB + pidx(dt + NC)) = pcd;
     }
-    if (d >= NC - MH) {
-      *reinterpret_cast<uint32_t*>(ra + b7idx(d - NC)) = wab;
-      *reinterpret_cast<uint32_t*>(rc + b7idx(d - NC)) = wcd;
+    if (halo_hi) {
+      *reinterpret_cast<uint32_t*>(rp + pidx(dt - NC)) = pab;
+      *reinterpret_cast<uint32_t*>(rp + RB + pidx(dt - NC)) = pcd;
     }
-    *reinterpret_cast<uint16_t*>(code + x * CS + d / 2) = (uint16_t)lv_cut_code(kw, Wc);
+    *reinterpret_cast<uint16_t*>(rp + 2 * RB + dt / 2) = (uint16_t)lv_cut_code(kw, Wc);
   };
 
   for (int g = blockIdx.x; g < n_strips; g += gridDim.x) {
     const int f = g % nf;
     const int t_beg = (g / nf) * steps, t_end = min(t_beg + steps, wg_per_frame);
     const float* fm = map + (size_t)f * ns * NC;
+    // the frame's map: rows off it (negative offsets wrap) read as zero by the range check
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(fm), (short)0, ns * NC * 4, 0x00020000);
+    auto load_row = [&](int row) {  // cells dt .. dt + 3 of map row `row` (uniform)
+      return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(row * (NC * 4) + 4 * dt), 0, 0));
+    };
     int base = 0;  // ring slot of tile row 0
-    float4 pre[4];
+    float4 pre[TR];
     const bool up = kK3AltDir && ((g / nf) & 1);  // odd strips walk upwards, as k_cfar2d's
+    const int xo = up ? 0 : 1;
     for (int k = 0; k < t_end - t_beg; ++k) {
       const int t = up ? t_end - 1 - k : t_beg + k;
       const bool first = k == 0, last = k + 1 == t_end - t_beg;
       const int wt0 = t * WPB;
       const int n_wt = min(WPB, wt_per_frame - wt0);
       const int r0 = wt0 * WR;
-      const int rlw = wv * WR + lane / TPR;
-      const int d0 = (lane % TPR) * 16;
-      const int r = r0 + rlw;
+      const int r = r0 + wv;
       __syncthreads();  // the previous step's waves are done with the rows
       if (first) {
         // levels: the mean key7 level of the first step's CUT rows (this thread's 16 cells), then the
         // kK3LvQA / _QB quantiles of a 128-bin histogram around it
-        float4 v[4];
+        float4 v[TR];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          int i, d;
-          blk(u, i, d);
-          v[u] = r0 + i < ns ? *reinterpret_cast<const float4*>(fm + (size_t)(r0 + i) * NC + d)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+        for (int u = 0; u < TR; ++u) v[u] = load_row(r0 + u);
         if (threadIdx.x == 0) cnt[12] = 0u;
         if (threadIdx.x < 128) hist[threadIdx.x] = 0u;
         uint32_t k7[16];
@@ -1085,8 +1083,9 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
           }
         }
         __syncthreads();
-        const uint32_t QA = (uint32_t)min(max((h0 + (int)cnt[14]) * 8, 1), 0x7f80);
-        const uint32_t QB = (uint32_t)min(max((h0 + (int)cnt[15]) * 8, 1), 0x7f80);
+        const int h0u = __builtin_amdgcn_readfirstlane(h0);
+        const uint32_t QA = (uint32_t)min(max((h0u + (int)__builtin_amdgcn_readfirstlane(cnt[14])) * 8, 1), 0x7f80);
+        const uint32_t QB = (uint32_t)min(max((h0u + (int)__builtin_amdgcn_readfirstlane(cnt[15])) * 8, 1), 0x7f80);
         // C / D one and two octaves above QB (exact: key16 + 128 doubles lo); the scale rules need them
         // inside the finite range and no scale override
         const bool s2ok = !a.override_ && QB + 256u < 0x7f80u;
@@ -1101,55 +1100,58 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
         ruleA = s2ok && key_lo(QB) <= 1.5f * key_lo(QA);
         const uint32_t U[4] = {UA, UB, U2A, U2B};
 #pragma unroll
-        for (int k = 0; k < 4; ++k) Wc[k] = ((U[k] | 0x8000u) - 1u) * 0x00010001u;
-        // the whole ring: rows r0 - hr .. r0 + TR + hr - 1 (zero outside the map), 4 float4 in flight
+        for (int k2 = 0; k2 < 4; ++k2) Wc[k2] = ((U[k2] | 0x8000u) - 1u) * 0x00010001u;
+        // the whole ring in walk order (tile rows 0 .. NR - 1 downwards, NR - 1 .. 0 upwards), 4 rows'
+        // loads in flight; the prefixes start at the strip's first row
         base = 0;
-        constexpr int n4 = NR * (NC / 4);
-        for (int b = tid; b < n4; b += 4 * NT) {
+        pab = pcd = 0u;
+#pragma unroll
+        for (int j0 = 0; j0 < NR; j0 += 4) {
           float4 w[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            const int e4 = b + u * NT;
-            const int x = e4 / (NC / 4), d = (e4 - x * (NC / 4)) * 4;
-            const int rr = r0 - HR + x;
-            w[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (e4 < n4 && rr >= 0 && rr < ns) w[u] = *reinterpret_cast<const float4*>(fm + (size_t)rr * NC + d);
+            const int x = up ? NR - 1 - (j0 + u) : j0 + u;
+            if (j0 + u < NR) w[u] = load_row(r0 - HR - xo + x);
           }
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int e4 = b + u * NT;
-            const int x = e4 / (NC / 4), d = (e4 - x * (NC / 4)) * 4;
-            if (e4 < n4) put(x, d, w[u]);
-          }
+          for (int u = 0; u < 4; ++u)
+            if (j0 + u < NR) stage(up ? NR - 1 - (j0 + u) : j0 + u, w[u]);
         }
       } else {
-        // the ring turns by TR rows; the TR new rows (prefetched) go into the slots of the rows that
-        // left: tile rows NR - TR .. (downwards) or 0 .. TR - 1 (upwards)
+        // the ring turns by TR rows; the TR new rows (prefetched in walk order) go into the slots of the
+        // rows that left: tile rows NR - TR .. NR - 1 (downwards) or TR - 1 .. 0 (upwards)
         base += up ? NR - TR : TR;
         if (base >= NR) base -= NR;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          int i, d;
-          blk(u, i, d);
-          int x = (up ? 0 : NR - TR) + i + base;
+        for (int j = 0; j < TR; ++j) {
+          int x = (up ? TR - 1 - j : NR - TR + j) + base;
           x = x >= NR ? x - NR : x;
-          put(x, d, pre[u]);
+          stage(x, pre[j]);
         }
       }
-      if (!last) {  // prefetch the next step's new rows: r0 + TR + hr .. or r0 - TR - hr .. (zero off the map)
+      if (!last) {  // prefetch the next step's new rows in walk order: r0 + TR + HR + j or r0 - HR - 1 - j
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          int i, d;
-          blk(u, i, d);
-          const int rr = (up ? r0 - TR - HR : r0 + TR + HR) + i;
-          pre[u] = rr >= 0 && rr < ns ? *reinterpret_cast<const float4*>(fm + (size_t)rr * NC + d)
-                                      : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+        for (int j = 0; j < TR; ++j) pre[j] = load_row(up ? r0 - HR - 1 - j : r0 + TR + HR + j);
       }
       __syncthreads();
       const bool has_tile = wv < n_wt;
       uint32_t surv = 0;
-      if (has_tile && r >= HR && r < ns - HR) surv = cfar2d_screen_rules<NC, HR, GR>(ab, cd, code, base, rlw, d0, need, ruleA);
+      if (has_tile && r >= HR && r < ns - HR) {
+        auto slot = [&](int x) {
+          const int y = x + base;
+          return y >= NR ? y - NR : y;
+        };
+        const uint8_t* const p_lo = ring + slot(wv) * ROWB + d0;                // pidx(d0 - 8) = d0
+        const uint8_t* const p_hi = ring + slot(wv + 2 * HR + 1) * ROWB + d0;
+        const uint8_t* const g_lo = ring + slot(wv + HR - GR) * ROWB + d0;
+        const uint8_t* const g_hi = ring + slot(wv + HR + GR + 1) * ROWB + d0;
+        const uint2 cw = *reinterpret_cast<const uint2*>(ring + slot(wv + HR + xo) * ROWB + 2 * RB + d0 / 2);
+        const uint8_t* const hA = up ? p_lo : p_hi;
+        const uint8_t* const lA = up ? p_hi : p_lo;
+        const uint8_t* const hG = up ? g_lo : g_hi;
+        const uint8_t* const lG = up ? g_hi : g_lo;
+        surv = cfar2d_screen_prefix<HR, GR>(hA, lA, hA + RB, lA + RB, hG, lG, cw, need, ruleA);
+      }
       // emission: each wave tile's survivors, in (range, doppler) order, as one run of the strip
       // buffer (flushed to the candidate list when full and at the strip's end); an empty tile is
       // final here.  (wg_base, wg_count) = (run start, run length) until k_cfar2d_emit.

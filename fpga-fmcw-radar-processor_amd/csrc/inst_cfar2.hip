@@ -8,7 +8,7 @@ namespace fmcw {
 // kernel (runtime window, pair screen, candidate test).  Of the two level-screen kernels, k_cfar2d
 // (key16 rows + in-launch candidate test) runs where its ring fits 4 workgroups per CU (<= 40 KB of
 // LDS: NC <= 512), k_cfar2d_lv (scale rules, 2.5 B per cell, no candidate test) where it does not
-// (NC = 1024: 46.7 KB, 3 workgroups per CU).  Measured (tools/cfar2d_bench.py, 16 frames, us per
+// (NC = 1024: 46.7 KB, 3 workgroups per CU; k_cfar2d_lv 40.7 KB, 4).  Measured (tools/cfar2d_bench.py, 16 frames, us per
 // launch, profiles/r05/k3_rules/): config 5 k_cfar2d 350, k_cfar2d_lv 297-302; config 3 k_cfar2d
 // 73, k_cfar2d_lv 95-100 (its 4-rx NCI cells pass the s_min screen rarely: the rules' extra screen
 // work buys nothing there).
@@ -18,9 +18,18 @@ constexpr bool rules_kernel() { return cfar2d_smem_bytes<N>(5) > 40 * 1024; }
 
 template <int N>
 static Cfar2Info info_t(bool lv, int hr) {
-  constexpr bool R = rules_kernel<N>();
-  Cfar2Fn fn = !lv ? k_cfar2d<N, 0, 0> : R ? k_cfar2d_lv<N, 5, 1> : k_cfar2d<N, 6, 2, 5, 1>;
-  const size_t smem = !lv ? cfar2d_smem_bytes<N>(hr) : R ? cfar2d_lv_smem_bytes<N, 5, 1>() : cfar2d_smem_bytes<N>(5);
+  Cfar2Fn fn = k_cfar2d<N, 0, 0>;
+  size_t smem = cfar2d_smem_bytes<N>(hr);
+  if (lv) {
+    if constexpr (rules_kernel<N>()) {
+      static_assert(N == 1024, "k_cfar2d_lv stages one 4-cell column per thread (NC = 1024)");
+      fn = k_cfar2d_lv<N, 5, 1>;
+      smem = cfar2d_lv_smem_bytes<N, 5, 1>();
+    } else {
+      fn = k_cfar2d<N, 6, 2, 5, 1>;
+      smem = cfar2d_smem_bytes<N>(5);
+    }
+  }
   return {fn, Cfar2DGeom<N>::TR, k_cfar2d_decide<N>, k_cfar2d_emit<N>, smem};
 }
 
