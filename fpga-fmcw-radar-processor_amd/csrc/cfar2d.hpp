@@ -160,6 +160,13 @@ __device__ __forceinline__ uint32_t lv_nibbles(uint2 kw, uint32_t qa2, uint32_t 
   const uint32_t pb = __builtin_amdgcn_perm(x1 - qb2, x0 - qb2, 0x07050301u);
   return ((pa >> 7) & 0x01010101u) | ((pb >> 3) & 0x10101010u);
 }
+// the same from sanitised keys (k <= 0x7f80) with ca2 / cb2 = (0x8000 - Q) in both halves: k + 0x8000 - Q
+// has bit 15 set iff k >= Q and stays below 0x10000 (no carry into the upper half)
+__device__ __forceinline__ uint32_t lv_nibbles_add(uint2 kw, uint32_t ca2, uint32_t cb2) {
+  const uint32_t pa = __builtin_amdgcn_perm(kw.y + ca2, kw.x + ca2, 0x07050301u);
+  const uint32_t pb = __builtin_amdgcn_perm(kw.y + cb2, kw.x + cb2, 0x07050301u);
+  return ((pa >> 7) & 0x01010101u) | ((pb >> 3) & 0x10101010u);
+}
 // byte-wise inclusive prefix sums of a word (bytes <= 63: no carry)
 __device__ __forceinline__ uint32_t byte_prefix(uint32_t x) {
   x += x << 8;
@@ -867,8 +874,10 @@ __device__ __forceinline__ uint32_t cfar2d_screen_prefix(const uint8_t* hiA, con
 #pragma unroll
     for (int k = 0; k < 6; ++k) G[k] = nib_sub(Gh[k + 1], Gl[k + 1]);
   }
-  // 13-cell window sums per level (bytes: cell d0 + 4m + t in word m byte t)
-  uint32_t HA[4], HB[4], HC[4], HD[4];
+  // 13-cell window sums per level (bytes: cell d0 + 4m + t in word m byte t); level D only as "any cell
+  // of the lane's whole 11 x 32 window at D" (a superset of every CUT's box: the rules hold as well with
+  // it; D cells are far out in the clutter's tail, so the survivors do not change on the bench maps)
+  uint32_t HA[4], HB[4], HC[4];
   {
     uint32_t XA[7], XB[7];
 #pragma unroll
@@ -880,14 +889,11 @@ __device__ __forceinline__ uint32_t cfar2d_screen_prefix(const uint8_t* hiA, con
     lv_sum13(XA, HA);
     lv_sum13(XB, HB);
 #pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      const uint32_t w = __builtin_amdgcn_alignbyte(W[k + 1], W[k], 2);
-      XA[k] = w & 0x0F0F0F0Fu;
-      XB[k] = (w >> 4) & 0x0F0F0F0Fu;
-    }
+    for (int k = 0; k < 7; ++k) XA[k] = __builtin_amdgcn_alignbyte(W[k + 1], W[k], 2) & 0x0F0F0F0Fu;
     lv_sum13(XA, HC);
-    lv_sum13(XB, HD);
   }
+  const uint32_t orD = (W[0] | W[1] | W[2] | W[3] | W[4] | W[5] | W[6] | W[7]) & 0xF0F0F0F0u;
+  const uint32_t okD = orD ? 0u : 0x80808080u;  // bit 7: no D cell in the window (lane-uniform)
   // guard block (3 x 5 around the CUT) of levels A / B in the nibbles
   uint32_t H5[4];
   {
@@ -904,27 +910,29 @@ __device__ __forceinline__ uint32_t cfar2d_screen_prefix(const uint8_t* hiA, con
   constexpr uint32_t H = 0x80808080u;
   auto K = [](int v) { return (uint32_t)v * 0x01010101u; };
   const uint32_t k_need = K(128 - need);
+  const uint32_t okA = ruleA ? okD : 0u;
+  // the CUTs' code nibbles as bytes: word m byte t = cell 4m + t's code
+  const uint32_t cx4 = cw.x >> 4, cy4 = cw.y >> 4;
   uint32_t bits = 0;
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
-    const uint32_t h16 = ((m < 2 ? cw.x : cw.y) >> (16 * (m & 1))) & 0xffffu;
-    const uint32_t e = __builtin_amdgcn_perm(h16, h16, 0x01010000u);       // bytes lo, lo, hi, hi
-    const uint32_t nb = (e & 0x000f000fu) | ((e >> 4) & 0x0f000f00u);      // byte t: cell 4m + t's code
+    const uint32_t src = m < 2 ? cw.x : cw.y, s4 = m < 2 ? cx4 : cy4;
+    // bytes (b, b >> 4, b', b' >> 4) of code bytes b = 2 (m & 1), b' = b + 1, then the low nibbles
+    const uint32_t nb = __builtin_amdgcn_perm(src, s4, (m & 1) ? 0x03070206u : 0x01050004u) & 0x0F0F0F0Fu;
     const uint32_t CA = HA[m] - (H5[m] & 0x0F0F0F0Fu), CB = HB[m] - ((H5[m] >> 4) & 0x0F0F0F0Fu);
-    const uint32_t CC = HC[m], CD = HD[m];
+    const uint32_t CC = HC[m];
     const uint32_t na = CA + k_need, nb2 = CB + k_need;                     // bit 7: C_A / C_B >= need
     const uint32_t smin = (na & (nb << 7)) | (nb2 & (nb << 6));             // E(s_min) >= need at A or B
-    const uint32_t nzD = ((CD & 0x7f7f7f7fu) + 0x7f7f7f7fu) | CD;           // bit 7: C_D != 0
-    const uint32_t rB = nb2 & ~(CB + K(64)) & ~(CC + K(95)) & ~nzD & (nb << 4);
-    uint32_t rA = na & ~(CA + K(47)) & ~(CB + K(87)) & ~((CC & 0x7f7f7f7fu) + K(119)) & ~nzD & (nb << 5);
-    if (!ruleA) rA = 0u;
+    const uint32_t rB = nb2 & ~(CB + K(64)) & ~(CC + K(95)) & okD & (nb << 4);
+    const uint32_t rA = na & ~(CA + K(47)) & ~(CB + K(87)) & ~((CC & 0x7f7f7f7fu) + K(119)) & okA & (nb << 5);
     const uint32_t surv = ~(smin | rA | rB) & H;
     bits |= ((surv * 0x00204081u) >> 28) << (4 * m);  // bit 7 of byte t -> bit 28 + t
   }
   return bits;
 }
 
-// k_cfar2d_lv at NC = 1024: thread t stages cells 4t .. 4t + 3 of every ring row (NC / 4 = NT), so
+// k_cfar2d_lv at NC = 1024 (CMP: the RTL-compat 17-bit integer cells, a.compat, as a template
+// switch: the staging's per-row branch cost copies): thread t stages cells 4t .. 4t + 3 of every ring row (NC / 4 = NT), so
 // it carries its column's two running prefixes from row to row in registers.  Ring tile row x is
 // map row r0 - HR - xo + x (xo = 1 walking downwards, 0 upwards: the extra row lies on the side the
 // prefix starts from); the strip's first step stages all NR rows in walk order, every later step
@@ -932,7 +940,7 @@ __device__ __forceinline__ uint32_t cfar2d_screen_prefix(const uint8_t* hiA, con
 // off the map).  For CUT row rl the window's column counts are P[rl + 2 HR + 1] - P[rl] (downwards;
 // upwards the prefix runs the other way and the difference flips), the guard rows'
 // P[rl + HR + GR + 1] - P[rl + HR - GR], the CUT row is tile row rl + HR + xo.
-template <int NC, int HR, int GR>
+template <int NC, int HR, int GR, bool CMP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int frame0, int tile0, Cfar2DArgs a,
             DetSink sink, Cfar2Cands cands) {
@@ -991,15 +999,20 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
   uint32_t pab = 0, pcd = 0;  // this column's running prefixes (A / B, C / D)
   // one ring slot's cells dt .. dt + 3: level bits into the prefixes, prefixes and cut codes to LDS
   auto stage = [&](int slot, float4 v) {
-    if (a.compat) v = q17x4(v);
+#if defined(FMCW_K3_ABL) && FMCW_K3_ABL == 2  // lab: no staging work (timing only)
+    asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+    (void)slot;
+    return;
+#endif
+    if constexpr (CMP) v = q17x4(v);
     // key16 without the NaN / negative cells (-> 0): a sign or NaN bit pattern is above inf's
     const uint32_t b0 = __float_as_uint(v.x), b1 = __float_as_uint(v.y), b2 = __float_as_uint(v.z),
                    b3 = __float_as_uint(v.w);
     const uint32_t s0 = b0 <= 0x7f800000u ? b0 : 0u, s1 = b1 <= 0x7f800000u ? b1 : 0u;
     const uint32_t s2 = b2 <= 0x7f800000u ? b2 : 0u, s3 = b3 <= 0x7f800000u ? b3 : 0u;
     const uint2 kw = make_uint2(__builtin_amdgcn_perm(s1, s0, 0x07060302u), __builtin_amdgcn_perm(s3, s2, 0x07060302u));
-    pab = nib_add(pab, lv_nibbles(kw, qa2, qb2));
-    pcd = nib_add(pcd, lv_nibbles(kw, qc2, qd2));
+    pab = nib_add(pab, lv_nibbles_add(kw, qa2, qb2));
+    pcd = nib_add(pcd, lv_nibbles_add(kw, qc2, qd2));
     uint8_t* const rp = ring + slot * ROWB;
     *reinterpret_cast<uint32_t*>(rp + pidx(dt)) = pab;
     *reinterpret_cast<uint32_t*>(rp + RB + pidx(dt)) = pcd;
@@ -1048,7 +1061,7 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
         uint32_t sum = 0;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const float4 w = a.compat ? q17x4(v[u]) : nonneg4(v[u]);
+          const float4 w = CMP ? q17x4(v[u]) : nonneg4(v[u]);
           k7[4 * u] = key16(w.x) >> 3;
           k7[4 * u + 1] = key16(w.y) >> 3;
           k7[4 * u + 2] = key16(w.z) >> 3;
@@ -1090,10 +1103,10 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
         // inside the finite range and no scale override
         const bool s2ok = !a.override_ && QB + 256u < 0x7f80u;
         const uint32_t QC = min(QB + 128u, 0x7f80u), QD = min(QB + 256u, 0x7f80u);
-        qa2 = QA | (QA << 16);
-        qb2 = QB | (QB << 16);
-        qc2 = QC | (QC << 16);
-        qd2 = QD | (QD << 16);
+        qa2 = (0x8000u - QA) * 0x00010001u;  // lv_nibbles_add's level constants
+        qb2 = (0x8000u - QB) * 0x00010001u;
+        qc2 = (0x8000u - QC) * 0x00010001u;
+        qd2 = (0x8000u - QD) * 0x00010001u;
         const float s2 = fminf(a.sc_nom, a.sc_max);
         const uint32_t UA = key16(a.s_min * key_lo(QA)), UB = key16(a.s_min * key_lo(QB));
         const uint32_t U2A = s2ok ? key16(s2 * key_lo(QA)) : 0u, U2B = s2ok ? key16(s2 * key_lo(QB)) : 0u;
@@ -1136,7 +1149,11 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
       __syncthreads();
       const bool has_tile = wv < n_wt;
       uint32_t surv = 0;
+#if defined(FMCW_K3_ABL) && FMCW_K3_ABL == 1  // lab: no screen (timing only)
+      if (false) {
+#else
       if (has_tile && r >= HR && r < ns - HR) {
+#endif
         auto slot = [&](int x) {
           const int y = x + base;
           return y >= NR ? y - NR : y;
@@ -1152,6 +1169,10 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
         const uint8_t* const lG = up ? g_hi : g_lo;
         surv = cfar2d_screen_prefix<HR, GR>(hA, lA, hA + RB, lA + RB, hG, lG, cw, need, ruleA);
       }
+#if defined(FMCW_K3_ABL) && FMCW_K3_ABL >= 2  // lab: the screen's result sunk (timing only)
+      asm volatile("" ::"v"(surv));
+      surv = 0;
+#endif
       // emission: each wave tile's survivors, in (range, doppler) order, as one run of the strip
       // buffer (flushed to the candidate list when full and at the strip's end); an empty tile is
       // final here.  (wg_base, wg_count) = (run start, run length) until k_cfar2d_emit.

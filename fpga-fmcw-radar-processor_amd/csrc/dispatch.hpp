@@ -64,6 +64,6 @@ struct Cfar2Info {
   Cfar2EmitFn emit;     // K3c k_cfar2d_emit
   size_t smem;          // K3a's dynamic LDS bytes
 };
-Cfar2Info cfar2_info(uint32_t nc, int hd, int gd, int hr, int gr);  // inst_cfar2.hip
+Cfar2Info cfar2_info(uint32_t nc, int hd, int gd, int hr, int gr, bool compat);  // inst_cfar2.hip
 
 }  // namespace fmcw

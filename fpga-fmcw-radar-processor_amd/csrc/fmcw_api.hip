@@ -379,7 +379,7 @@ int validate(const fmcw_config& c) {
       return fail(FMCW_EINVAL, "2-D CFAR window wider than n_doppler");
     if (c.cfar2d_scale_override > 7)
       return fail(FMCW_EINVAL, "scale_override is a 3-bit port (0..7)");
-    if (cfar2_info(c.n_doppler, a.hd, a.gd, a.hr, a.gr).smem > 160 * 1024)
+    if (cfar2_info(c.n_doppler, a.hd, a.gd, a.hr, a.gr, a.compat != 0).smem > 160 * 1024)
       return fail(FMCW_EINVAL, "2-D CFAR range extent too large for LDS");
   } else if (c.cfar_kind != FMCW_CFAR_NONE) {
     return fail(FMCW_EINVAL, "cfar_kind=%d unknown", c.cfar_kind);
@@ -571,7 +571,7 @@ int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipS
   const int tile0 = (int)(frame0 * tiles_per_frame(h));
   if (c.cfar_kind == FMCW_CFAR_OS2D) {
     const Cfar2DArgs a = cfar2_args(c);
-    const Cfar2Info ci = cfar2_info(c.n_doppler, a.hd, a.gd, a.hr, a.gr);
+    const Cfar2Info ci = cfar2_info(c.n_doppler, a.hd, a.gd, a.hr, a.gr, a.compat != 0);
     const size_t frame_px = (size_t)c.n_range * c.n_doppler;
     // pieces of at most k3_frames frames (the candidate lists' capacity), each its own K3a/b/c
     for (int p0 = 0; p0 < nf; p0 += h->k3_frames) {
@@ -845,7 +845,7 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   }
   if (c.cfar_kind == FMCW_CFAR_OS2D) {
     const Cfar2DArgs a = cfar2_args(c);
-    const Cfar2Info ci = cfar2_info(c.n_doppler, a.hd, a.gd, a.hr, a.gr);  // the kernel launch_cfar runs
+    const Cfar2Info ci = cfar2_info(c.n_doppler, a.hd, a.gd, a.hr, a.gr, a.compat != 0);  // the kernel launch_cfar runs
     h->cfar2d_smem = ci.smem;
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(ci.fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)h->cfar2d_smem) != hipSuccess)

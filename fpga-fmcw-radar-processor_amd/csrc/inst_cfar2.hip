@@ -17,13 +17,13 @@ template <int N>
 constexpr bool rules_kernel() { return cfar2d_smem_bytes<N>(5) > 40 * 1024; }
 
 template <int N>
-static Cfar2Info info_t(bool lv, int hr) {
+static Cfar2Info info_t(bool lv, int hr, bool compat) {
   Cfar2Fn fn = k_cfar2d<N, 0, 0>;
   size_t smem = cfar2d_smem_bytes<N>(hr);
   if (lv) {
     if constexpr (rules_kernel<N>()) {
       static_assert(N == 1024, "k_cfar2d_lv stages one 4-cell column per thread (NC = 1024)");
-      fn = k_cfar2d_lv<N, 5, 1>;
+      fn = compat ? k_cfar2d_lv<N, 5, 1, true> : k_cfar2d_lv<N, 5, 1, false>;
       smem = cfar2d_lv_smem_bytes<N, 5, 1>();
     } else {
       fn = k_cfar2d<N, 6, 2, 5, 1>;
@@ -33,10 +33,10 @@ static Cfar2Info info_t(bool lv, int hr) {
   return {fn, Cfar2DGeom<N>::TR, k_cfar2d_decide<N>, k_cfar2d_emit<N>, smem};
 }
 
-Cfar2Info cfar2_info(uint32_t nc, int hd, int gd, int hr, int gr) {
+Cfar2Info cfar2_info(uint32_t nc, int hd, int gd, int hr, int gr, bool compat) {
   const bool lv = lv_window(hd, gd, hr, gr);
   switch (nc) {
-#define C_(N) case N: return info_t<N>(lv, hr);
+#define C_(N) case N: return info_t<N>(lv, hr, compat);
     C_(32) C_(64) C_(128) C_(256) C_(512) C_(1024)
 #undef C_
   }
