@@ -1251,17 +1251,38 @@ k_cfar2d_decide(const float* __restrict__ map, int ns, Cfar2DArgs a, Cfar2Cands 
   const int need = a.n_ref - a.rank;
   const uint32_t n = cands.ctr[0];
   const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
-  auto cell = [&](uint32_t i) {
-    const float v = map[i];
-    return a.compat ? q17(v) : nonneg(v);
+  auto cell = [&](float v) { return a.compat ? q17(v) : nonneg(v); };
+  // Software-pipelined (round 5): the next candidate's cut and refs are in flight while this one is
+  // decided, the one after next's cell index a step earlier still (the refs' addresses depend on it);
+  // the windows mostly come from HBM / MALL again, K3a having streamed the launch's frames through.
+  struct Pend {
+    float cut, va, vb;
   };
-  for (uint32_t i = w0; i < n; i += nw) {
-    const uint32_t c = cands.cell[i];                     // (f ns + r) NC + d
-    const uint32_t fr = c / (uint32_t)NC, d = c & (uint32_t)(NC - 1);  // fr = f ns + r
-    const float cut = cell(c);
-    // refs: rows r + dr stay inside the frame (a CUT row has its whole range extent inside it)
-    const float va = oka ? cell((fr + dra) * (uint32_t)NC + ((d + dda) & (uint32_t)(NC - 1))) : 0.f;
-    const float vb = okb ? cell((fr + drb) * (uint32_t)NC + ((d + ddb) & (uint32_t)(NC - 1))) : 0.f;
+  // (branch-free: lanes past n_ref read their row's first cell and the last candidate stands in past
+  // the list's end, so the waits can count the loads in flight)
+  auto fetch = [&](uint32_t c) {  // c = (f ns + r) NC + d; rows r + dr stay inside the frame
+    const uint32_t fr = c / (uint32_t)NC, d = c & (uint32_t)(NC - 1);
+    Pend p;
+    p.cut = map[c];  // c in a VGPR (opaque below): a vector load, counted with the refs'
+    p.va = map[oka ? (fr + dra) * (uint32_t)NC + ((d + dda) & (uint32_t)(NC - 1)) : fr * (uint32_t)NC];
+    p.vb = map[okb ? (fr + drb) * (uint32_t)NC + ((d + ddb) & (uint32_t)(NC - 1)) : fr * (uint32_t)NC];
+    return p;
+  };
+  // the loop counter is scalar; the cell indices are read by vector loads (opaque lane offsets), so
+  // that the shuffles' LDS waits do not also wait for them
+  uint32_t i = __builtin_amdgcn_readfirstlane(w0);
+  if (i >= n) return;
+  const uint32_t* const cl = cands.cell;
+  uint32_t c_next = cl[opaque(0) + min(i + nw, n - 1)];
+  Pend cur = fetch(cl[opaque(0) + i]);
+  for (; i < n; i += nw) {
+    const uint32_t c_after = cl[opaque(0) + min(i + 2 * nw, n - 1)];
+    const Pend nxt = fetch(c_next);
+    const float cut = cell(cur.cut);
+    const float va = oka ? cell(cur.va) : 0.f;
+    const float vb = okb ? cell(cur.vb) : 0.f;
+    cur = nxt;
+    c_next = c_after;
     float sum = va + vb;
 #pragma unroll
     for (int x = 32; x >= 1; x >>= 1) sum += __shfl_xor(sum, x, 64);
@@ -1295,44 +1316,70 @@ k_cfar2d_decide(const float* __restrict__ map, int ns, Cfar2DArgs a, Cfar2Cands 
 }
 
 // ---- K3c: per wave tile with candidates, its detections in order into the sink (det_reserve_wave:
-// the tile's slot, or the overflow region), 64 candidates per round.
+// the tile's slot, or the overflow region).  One lane per tile first (round 5): most tiles' few
+// candidates were all rejected, and such a tile is final with (slot, 0) -- a wave per tile spent
+// three dependent loads on each.  Tiles with detections, or with more than kEmitLaneRun candidates,
+// then go through the whole wave one after the other, 64 candidates per round.
+constexpr uint32_t kEmitLaneRun = 8;
 template <int NC>
 __global__ void __launch_bounds__(256)
 k_cfar2d_emit(const float* __restrict__ map, int ns, int frame0, Cfar2DArgs a, Cfar2Cands cands, DetSink sink) {
   const int lane = threadIdx.x & 63;
   const uint32_t nt = cands.ctr[1];
   const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
-  for (uint32_t ti = w0; ti < nt; ti += nw) {
-    const int tile = (int)cands.tiles[ti];
-    const uint32_t p0 = sink.wg_base[tile], k = sink.wg_count[tile];  // the candidate run (k_cfar2d)
-    int total = 0;
-    for (uint32_t j0 = 0; j0 < k; j0 += 64) {
-      const bool det = j0 + lane < k && cands.thr[p0 + j0 + lane] >= 0.f;
-      total += (int)__popcll(__ballot(det));
-    }
-    const uint32_t base = det_reserve_wave(sink, tile, total);
-    uint32_t o = base;
-    for (uint32_t j0 = 0; j0 < k; j0 += 64) {
-      const uint32_t j = j0 + lane;
-      const float thr = j < k ? cands.thr[p0 + j] : -1.f;
-      const uint64_t bal = __ballot(thr >= 0.f);
-      if (thr >= 0.f) {
-        const uint32_t slot = o + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-        if (slot < sink.cap) {
-          const uint32_t c = cands.cell[p0 + j];
-          const uint32_t fr = c / (uint32_t)NC;
-          const float v = map[c];
-          fmcw_det dd;
-          dd.frame = (uint32_t)frame0 + fr / (uint32_t)ns;
-          dd.range = (uint16_t)(fr % (uint32_t)ns);
-          dd.doppler = (uint16_t)(c & (uint32_t)(NC - 1));
-          dd.mag = a.compat ? q17(v) : nonneg(v);
-          dd.threshold = thr;
-          sink.scratch[slot] = dd;
-        }
+  for (uint32_t t0 = w0 * 64u; t0 < nt; t0 += nw * 64u) {
+    const uint32_t ti = t0 + (uint32_t)lane;
+    int tile = 0;
+    uint32_t p0 = 0, k = 0;
+    bool wave = false;
+    if (ti < nt) {
+      tile = (int)cands.tiles[ti];
+      p0 = sink.wg_base[tile];  // the candidate run (k_cfar2d)
+      k = sink.wg_count[tile];
+      bool det = k > kEmitLaneRun;
+#pragma unroll
+      for (uint32_t j = 0; j < kEmitLaneRun; ++j)
+        if (j < k && !det) det = cands.thr[p0 + j] >= 0.f;
+      if (det) {
+        wave = true;
+      } else {
+        sink.wg_base[tile] = (uint32_t)tile * sink.slot_cap;
+        sink.wg_count[tile] = 0u;
       }
-      o += (uint32_t)__popcll(bal);
+    }
+    for (uint64_t m = __ballot(wave); m; m &= m - 1) {  // uniform
+      const int l = __builtin_ctzll(m);
+      const int tl = __shfl(tile, l, 64);
+      const uint32_t pl = (uint32_t)__shfl((int)p0, l, 64), kl = (uint32_t)__shfl((int)k, l, 64);
+      int total = 0;
+      for (uint32_t j0 = 0; j0 < kl; j0 += 64) {
+        const bool det = j0 + lane < kl && cands.thr[pl + j0 + lane] >= 0.f;
+        total += (int)__popcll(__ballot(det));
+      }
+      const uint32_t base = det_reserve_wave(sink, tl, total);
+      uint32_t o = base;
+      for (uint32_t j0 = 0; j0 < kl && total; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        const float thr = j < kl ? cands.thr[pl + j] : -1.f;
+        const uint64_t bal = __ballot(thr >= 0.f);
+        if (thr >= 0.f) {
+          const uint32_t slot = o + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+          if (slot < sink.cap) {
+            const uint32_t c = cands.cell[pl + j];
+            const uint32_t fr = c / (uint32_t)NC;
+            const float v = map[c];
+            fmcw_det dd;
+            dd.frame = (uint32_t)frame0 + fr / (uint32_t)ns;
+            dd.range = (uint16_t)(fr % (uint32_t)ns);
+            dd.doppler = (uint16_t)(c & (uint32_t)(NC - 1));
+            dd.mag = a.compat ? q17(v) : nonneg(v);
+            dd.threshold = thr;
+            sink.scratch[slot] = dd;
+          }
+        }
+        o += (uint32_t)__popcll(bal);
+      }
     }
   }
 }
