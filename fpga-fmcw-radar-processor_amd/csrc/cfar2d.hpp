@@ -1048,7 +1048,9 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
       const int n_wt = min(WPB, wt_per_frame - wt0);
       const int r0 = wt0 * WR;
       const int r = r0 + wv;
-      __syncthreads();  // the previous step's waves are done with the rows
+      // the previous step's waves are done with the rows: at a strip's start by the barrier after the
+      // last strip, later by the emission's barrier (every wave passes it after its screen)
+      if (first) __syncthreads();
       if (first) {
         // levels: the mean key7 level of the first step's CUT rows (this thread's 16 cells), then the
         // kK3LvQA / _QB quantiles of a 128-bin histogram around it
@@ -1327,8 +1329,10 @@ k_cfar2d_emit(const float* __restrict__ map, int ns, int frame0, Cfar2DArgs a, C
   const int lane = threadIdx.x & 63;
   const uint32_t nt = cands.ctr[1];
   const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
-  for (uint32_t t0 = w0 * 64u; t0 < nt; t0 += nw * 64u) {
-    const uint32_t ti = t0 + (uint32_t)lane;
+  // lane l of wave w takes list entries w + nw (l + 64 i): consecutive entries (a target's tiles,
+  // which carry the detections) go to different waves
+  for (uint32_t t0 = 0; t0 < nt; t0 += nw * 64u) {
+    const uint32_t ti = t0 + (uint32_t)lane * nw + w0;
     int tile = 0;
     uint32_t p0 = 0, k = 0;
     bool wave = false;
@@ -1337,9 +1341,11 @@ k_cfar2d_emit(const float* __restrict__ map, int ns, int frame0, Cfar2DArgs a, C
       p0 = sink.wg_base[tile];  // the candidate run (k_cfar2d)
       k = sink.wg_count[tile];
       bool det = k > kEmitLaneRun;
+      float t[kEmitLaneRun];
 #pragma unroll
-      for (uint32_t j = 0; j < kEmitLaneRun; ++j)
-        if (j < k && !det) det = cands.thr[p0 + j] >= 0.f;
+      for (uint32_t j = 0; j < kEmitLaneRun; ++j) t[j] = cands.thr[p0 + min(j, k - 1u)];  // k >= 1
+#pragma unroll
+      for (uint32_t j = 0; j < kEmitLaneRun; ++j) det |= t[j] >= 0.f;
       if (det) {
         wave = true;
       } else {
