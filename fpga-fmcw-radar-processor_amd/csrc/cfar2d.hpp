@@ -874,10 +874,12 @@ __device__ __forceinline__ uint32_t cfar2d_screen_prefix(const uint8_t* hiA, con
 #pragma unroll
     for (int k = 0; k < 6; ++k) G[k] = nib_sub(Gh[k + 1], Gl[k + 1]);
   }
-  // 13-cell window sums per level (bytes: cell d0 + 4m + t in word m byte t); level D only as "any cell
-  // of the lane's whole 11 x 32 window at D" (a superset of every CUT's box: the rules hold as well with
-  // it; D cells are far out in the clutter's tail, so the survivors do not change on the bench maps)
-  uint32_t HA[4], HB[4], HC[4];
+  // 13-cell window sums of levels A and B (bytes: cell d0 + 4m + t in word m byte t).  Levels C and D
+  // only enter the rules through upper bounds, so they are counted over supersets of the boxes (the
+  // rules hold as well with them): C over the 16 cells around each group of 4 CUTs, D as "any cell of
+  // the lane's whole 11 x 32 window at D".  On the bench maps (NumPy model of the rules) the survivors
+  // do not change: D cells lie far out in the clutter's tail, C cells are rare enough.
+  uint32_t HA[4], HB[4], okC32[4], okC8[4];
   {
     uint32_t XA[7], XB[7];
 #pragma unroll
@@ -888,9 +890,18 @@ __device__ __forceinline__ uint32_t cfar2d_screen_prefix(const uint8_t* hiA, con
     }
     lv_sum13(XA, HA);
     lv_sum13(XB, HB);
+    // C: word k byte t = cell d0 - 6 + 4k + t; group m's 13-cell boxes lie in words m .. m + 3
+    uint32_t XC[7], P2[6];
 #pragma unroll
-    for (int k = 0; k < 7; ++k) XA[k] = __builtin_amdgcn_alignbyte(W[k + 1], W[k], 2) & 0x0F0F0F0Fu;
-    lv_sum13(XA, HC);
+    for (int k = 0; k < 7; ++k) XC[k] = __builtin_amdgcn_alignbyte(W[k + 1], W[k], 2) & 0x0F0F0F0Fu;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) P2[k] = XC[k] + XC[k + 1];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const uint32_t g = __builtin_amdgcn_sad_u8(P2[m] + P2[m + 2], 0u, 0u);  // <= 176
+      okC32[m] = g <= 32u ? 0x80808080u : 0u;
+      okC8[m] = g <= 8u ? 0x80808080u : 0u;
+    }
   }
   const uint32_t orD = (W[0] | W[1] | W[2] | W[3] | W[4] | W[5] | W[6] | W[7]) & 0xF0F0F0F0u;
   const uint32_t okD = orD ? 0u : 0x80808080u;  // bit 7: no D cell in the window (lane-uniform)
@@ -913,20 +924,24 @@ __device__ __forceinline__ uint32_t cfar2d_screen_prefix(const uint8_t* hiA, con
   const uint32_t okA = ruleA ? okD : 0u;
   // the CUTs' code nibbles as bytes: word m byte t = cell 4m + t's code
   const uint32_t cx4 = cw.x >> 4, cy4 = cw.y >> 4;
-  uint32_t bits = 0;
+  uint32_t sv[4];
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
     const uint32_t src = m < 2 ? cw.x : cw.y, s4 = m < 2 ? cx4 : cy4;
     // bytes (b, b >> 4, b', b' >> 4) of code bytes b = 2 (m & 1), b' = b + 1, then the low nibbles
     const uint32_t nb = __builtin_amdgcn_perm(src, s4, (m & 1) ? 0x03070206u : 0x01050004u) & 0x0F0F0F0Fu;
     const uint32_t CA = HA[m] - (H5[m] & 0x0F0F0F0Fu), CB = HB[m] - ((H5[m] >> 4) & 0x0F0F0F0Fu);
-    const uint32_t CC = HC[m];
     const uint32_t na = CA + k_need, nb2 = CB + k_need;                     // bit 7: C_A / C_B >= need
     const uint32_t smin = (na & (nb << 7)) | (nb2 & (nb << 6));             // E(s_min) >= need at A or B
-    const uint32_t rB = nb2 & ~(CB + K(64)) & ~(CC + K(95)) & okD & (nb << 4);
-    const uint32_t rA = na & ~(CA + K(47)) & ~(CB + K(87)) & ~((CC & 0x7f7f7f7fu) + K(119)) & okA & (nb << 5);
-    const uint32_t surv = ~(smin | rA | rB) & H;
-    bits |= ((surv * 0x00204081u) >> 28) << (4 * m);  // bit 7 of byte t -> bit 28 + t
+    const uint32_t rB = nb2 & ~(CB + K(64)) & okC32[m] & okD & (nb << 4);   // C_B <= 63, C_C <= 32
+    const uint32_t rA = na & ~(CA + K(47)) & ~(CB + K(87)) & okC8[m] & okA & (nb << 5);  // 80, 40, 8
+    sv[m] = ~(smin | rA | rB) & H;
+  }
+  // the survivor bits in cell order, only where there are any (a few lanes in a thousand)
+  uint32_t bits = 0;
+  if (sv[0] | sv[1] | sv[2] | sv[3]) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) bits |= ((sv[m] * 0x00204081u) >> 28) << (4 * m);  // bit 7 of byte t -> bit 28 + t
   }
   return bits;
 }
@@ -1242,26 +1257,44 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
 // oracle tree_sum_f32); the scale bracket comes from ballot counts (ranked > M <=> #{ref > M} >=
 // n_ref - k; os_cfar_2d.vhd:189-213); detect <=> #{fl(s ref) >= cut} < n_ref - k; a detection's
 // ranked value (k-th smallest) by the pivoting select, threshold = fl(s ranked) (dbg_threshold).
-template <int NC>
-__global__ void __launch_bounds__(256)
-k_cfar2d_decide(const float* __restrict__ map, int ns, Cfar2DArgs a, Cfar2Cands cands) {
+// The fixed fp32 halving tree of a wave's values (xor partners 32, 16, .., 1: oracle tree_sum_f32),
+// every lane ending with the sum.  Steps 8 .. 1 are DPP row rotations: after the steps above it, the
+// lane a rotation by x reaches holds the xor partner's value bit for bit (fp32 addition commutes).
+__device__ __forceinline__ float wave_tree_sum(float s, int a32, int a16) {
+  s += __int_as_float(__builtin_amdgcn_ds_bpermute(a32, __float_as_int(s)));
+  s += __int_as_float(__builtin_amdgcn_ds_bpermute(a16, __float_as_int(s)));
+  s += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x128, 0xf, 0xf, false));  // row_ror:8
+  s += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x124, 0xf, 0xf, false));  // row_ror:4
+  s += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x122, 0xf, 0xf, false));  // row_ror:2
+  s += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x121, 0xf, 0xf, false));  // row_ror:1
+  return s;
+}
+__device__ __forceinline__ int ballot_count(bool p) { return __popcll(__builtin_amdgcn_ballot_w64(p)); }
+
+template <int NC, bool CMP>
+__device__ __forceinline__ void cfar2d_decide_run(const float* __restrict__ map, const Cfar2DArgs& a,
+                                                  const Cfar2Cands& cands) {
   const int lane = threadIdx.x & 63;
   int dra, dda, drb, ddb;
   cfar2d_ref_offset(a, lane, dra, dda);
   cfar2d_ref_offset(a, lane + 64, drb, ddb);
   const bool oka = lane < a.n_ref, okb = lane + 64 < a.n_ref;
   const int need = a.n_ref - a.rank;
+  const int a32 = (lane ^ 32) * 4, a16 = (lane ^ 16) * 4;
+  // fl(sum / n): with n a power of two the product with 1 / n is the same correctly rounded value
+  const bool n_pow2 = (a.n_ref & (a.n_ref - 1)) == 0;
+  const float inv_n = 1.0f / (float)a.n_ref;
   const uint32_t n = cands.ctr[0];
   const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
-  auto cell = [&](float v) { return a.compat ? q17(v) : nonneg(v); };
+  auto cell = [](float v) { return CMP ? q17(v) : nonneg(v); };
   // Software-pipelined (round 5): the next candidate's cut and refs are in flight while this one is
   // decided, the one after next's cell index a step earlier still (the refs' addresses depend on it);
   // the windows mostly come from HBM / MALL again, K3a having streamed the launch's frames through.
+  // (Branch-free: lanes past n_ref read their row's first cell and the last candidate stands in past
+  // the list's end, so the waits can count the loads in flight.)
   struct Pend {
     float cut, va, vb;
   };
-  // (branch-free: lanes past n_ref read their row's first cell and the last candidate stands in past
-  // the list's end, so the waits can count the loads in flight)
   auto fetch = [&](uint32_t c) {  // c = (f ns + r) NC + d; rows r + dr stay inside the frame
     const uint32_t fr = c / (uint32_t)NC, d = c & (uint32_t)(NC - 1);
     Pend p;
@@ -1285,28 +1318,26 @@ k_cfar2d_decide(const float* __restrict__ map, int ns, Cfar2DArgs a, Cfar2Cands 
     const float vb = okb ? cell(cur.vb) : 0.f;
     cur = nxt;
     c_next = c_after;
-    float sum = va + vb;
-#pragma unroll
-    for (int x = 32; x >= 1; x >>= 1) sum += __shfl_xor(sum, x, 64);
+    const float sum = wave_tree_sum(va + vb, a32, a16);
     float sc = (float)a.override_;
     if (!a.override_) {
       float half, hi;
-      if (a.compat) {
+      if constexpr (CMP) {
         // integer cells < 2^17, <= 128 of them: every partial sum < 2^24 is exact in fp32.
         // mean = floor(sum / N_REF) (os_cfar_2d.vhd:189); the bracket add is 17 bits wide (:193)
         const uint32_t mean = (uint32_t)sum / (uint32_t)a.n_ref;
         half = (float)(mean >> 1);
         hi = (float)((mean + (mean >> 1)) & kQ17Mask);
       } else {
-        const float mean = sum / (float)a.n_ref;
+        const float mean = n_pow2 ? sum * inv_n : sum / (float)a.n_ref;
         half = mean * 0.5f;
         hi = mean + half;
       }
-      const int n_hi = __popcll(__ballot(oka && va > hi)) + __popcll(__ballot(okb && vb > hi));
-      const int n_lo = __popcll(__ballot(oka && va < half)) + __popcll(__ballot(okb && vb < half));
+      const int n_hi = ballot_count(oka && va > hi) + ballot_count(okb && vb > hi);
+      const int n_lo = ballot_count(oka && va < half) + ballot_count(okb && vb < half);
       sc = (n_hi >= need) ? a.sc_max : (n_lo >= a.rank + 1) ? a.sc_min : a.sc_nom;
     }
-    const int n_ge = __popcll(__ballot(oka && sc * va >= cut)) + __popcll(__ballot(okb && sc * vb >= cut));
+    const int n_ge = ballot_count(oka && sc * va >= cut) + ballot_count(okb && sc * vb >= cut);
     float thr = -1.f;
     if (n_ge < need) {  // uniform
       const uint32_t ranked = wave_select_kth(oka ? __float_as_uint(va) : 0u, okb ? __float_as_uint(vb) : 0u,
@@ -1315,6 +1346,13 @@ k_cfar2d_decide(const float* __restrict__ map, int ns, Cfar2DArgs a, Cfar2Cands 
     }
     if (lane == 0) cands.thr[i] = thr;
   }
+}
+template <int NC>
+__global__ void __launch_bounds__(256)
+k_cfar2d_decide(const float* __restrict__ map, int ns, Cfar2DArgs a, Cfar2Cands cands) {
+  (void)ns;
+  if (a.compat) cfar2d_decide_run<NC, true>(map, a, cands);
+  else cfar2d_decide_run<NC, false>(map, a, cands);
 }
 
 // ---- K3c: per wave tile with candidates, its detections in order into the sink (det_reserve_wave:
