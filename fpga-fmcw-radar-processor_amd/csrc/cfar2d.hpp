@@ -1014,11 +1014,6 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
   uint32_t pab = 0, pcd = 0;  // this column's running prefixes (A / B, C / D)
   // one ring slot's cells dt .. dt + 3: level bits into the prefixes, prefixes and cut codes to LDS
   auto stage = [&](int slot, float4 v) {
-#if defined(FMCW_K3_ABL) && FMCW_K3_ABL == 2  // lab: no staging work (timing only)
-    asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-    (void)slot;
-    return;
-#endif
     if constexpr (CMP) v = q17x4(v);
     // key16 without the NaN / negative cells (-> 0): a sign or NaN bit pattern is above inf's
     const uint32_t b0 = __float_as_uint(v.x), b1 = __float_as_uint(v.y), b2 = __float_as_uint(v.z),
@@ -1166,11 +1161,7 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
       __syncthreads();
       const bool has_tile = wv < n_wt;
       uint32_t surv = 0;
-#if defined(FMCW_K3_ABL) && FMCW_K3_ABL == 1  // lab: no screen (timing only)
-      if (false) {
-#else
       if (has_tile && r >= HR && r < ns - HR) {
-#endif
         auto slot = [&](int x) {
           const int y = x + base;
           return y >= NR ? y - NR : y;
@@ -1186,10 +1177,6 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
         const uint8_t* const lG = up ? g_hi : g_lo;
         surv = cfar2d_screen_prefix<HR, GR>(hA, lA, hA + RB, lA + RB, hG, lG, cw, need, ruleA);
       }
-#if defined(FMCW_K3_ABL) && FMCW_K3_ABL >= 2  // lab: the screen's result sunk (timing only)
-      asm volatile("" ::"v"(surv));
-      surv = 0;
-#endif
       // emission: each wave tile's survivors, in (range, doppler) order, as one run of the strip
       // buffer (flushed to the candidate list when full and at the strip's end); an empty tile is
       // final here.  (wg_base, wg_count) = (run start, run length) until k_cfar2d_emit.
