@@ -268,6 +268,7 @@ struct fmcw_handle {
   size_t stage_dets_cap = 0;
   // grid sizes
   int grid_range = 0, grid_doppler = 0, grid_cfar = 0;
+  int grid_k3b = 0, grid_k3c = 0;       // K3b / K3c grids (kCfar2DecideGrid / kCfar2EmitGrid)
   size_t cfar2d_smem = 0;
   size_t inter_bytes = 0;               // h->inter (chunk frames of the K1 -> K2 spectrum)
   int cfar2_steps = 0;                  // 2-D CFAR steps per strip (0 = cost model; FMCW_PARAM_CFAR2D_STEPS)
@@ -561,7 +562,11 @@ constexpr size_t kCfar2Batch = 16;  // frames per 2-D CFAR launch on the caller'
 // Round 5, with k_cfar2d_lv's ~10^5 candidates per 16-frame launch at config 5 (tools/cfar2d_bench.py,
 // profiles/r05/k3_rules/): 1024 / 256 workgroups 336 us per launch, 2048 / 256 323, 2048 / 1024
 // 302, 4096 / 2048 297; with round 4's few thousand candidates the grid was measured neutral.
-constexpr int kCfar2DecideGrid = 2048;
+// After K3b's software pipeline (later in round 5; tools/k3_grid_ab.sh, profiles/r05/k3_grid/, two
+// interleaved passes, us per K3 batch, config 5 / config 3): 2048 / 1024 workgroups 261, 252 /
+// 75.6, 75.1; 1024 / 1024 258, 250 / 73.3, 72.3; 4096 / 1024 253, 255 / 81.7, 81.4; emit grids 256 /
+// 512 within noise.
+constexpr int kCfar2DecideGrid = 1024;
 constexpr int kCfar2EmitGrid = 1024;
 
 // The CFAR launcher shared by fmcw_enqueue (map just produced by K2) and fmcw_cfar.
@@ -591,8 +596,8 @@ int launch_cfar(fmcw_handle* h, const float* map_chunk, int nf, int frame0, hipS
                steps, frame0 + p0, tile0 + (int)(p0 * tiles_per_frame(h)), a, sink, cands);
       if (int rc = check_launch("k_cfar2d")) return rc;
       // K3b / K3c: fixed grids that read the candidate counts on the device (no host round trip)
-      launch_k(ps, false, ci.decide, dim3(kCfar2DecideGrid), dim3(256), 0u, s, mp, (int)c.n_range, a, cands);
-      launch_k(ps, true, ci.emit, dim3(kCfar2EmitGrid), dim3(256), 0u, s, mp, (int)c.n_range, frame0 + p0, a, cands,
+      launch_k(ps, false, ci.decide, dim3(h->grid_k3b), dim3(256), 0u, s, mp, (int)c.n_range, a, cands);
+      launch_k(ps, true, ci.emit, dim3(h->grid_k3c), dim3(256), 0u, s, mp, (int)c.n_range, frame0 + p0, a, cands,
                sink);
       if (int rc = check_launch("k_cfar2d_decide / _emit")) return rc;
     }
@@ -852,6 +857,8 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
       (void)hipGetLastError();
     occupancy_grid(ci.fn, 256, h->cfar2d_smem, h->n_cu, &h->grid_cfar);
   }
+  h->grid_k3b = kCfar2DecideGrid;
+  h->grid_k3c = kCfar2EmitGrid;
 #if FMCW_LAB
   // experiment knobs (tools/overlap_lab.py): cap a persistent grid so that another stream's
   // kernels find free CU slots beside it
@@ -864,6 +871,9 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
   cap_grid("FMCW_GRID_RANGE", &h->grid_range);
   cap_grid("FMCW_GRID_DOPPLER", &h->grid_doppler);
   cap_grid("FMCW_GRID_CFAR", &h->grid_cfar);
+  for (auto [name, g] : {std::pair<const char*, int*>{"FMCW_GRID_K3B", &h->grid_k3b}, {"FMCW_GRID_K3C", &h->grid_k3c}})
+    if (const char* v = std::getenv(name))
+      if (std::atoi(v) > 0) *g = std::atoi(v);
 #endif
   *out = h;
   return FMCW_OK;
