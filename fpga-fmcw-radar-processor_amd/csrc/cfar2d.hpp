@@ -149,6 +149,11 @@ constexpr size_t cfar2d_smem_bytes(int hr) {
 // screen's LDS reads in flight ahead of the accumulation (round 5: 2 or 3 measured alike, 2 keeps
 // k_cfar2d_lv spill-free at 4 waves per SIMD)
 constexpr int kK3LvQA = 560, kK3LvQB = 680, kK3ScreenAhead = 2;
+// k_cfar2d_lv's two levels (its scale rules change the optimum): the 50 % / 74 % quantiles, B clamped
+// to 1.5 A so that rule A stays available.  NumPy model of the rules on the config-5 bench map
+// (4 x 48 rows): survivors 0.0356 % at 56 / 68, 0.0041 % at 50 / 74; 48 / 76, where B passes 1.5 A
+// unclamped, 2.2 %.
+constexpr int kK3RulesQA = 500, kK3RulesQB = 740;
 // k_cfar2d: odd strips of a frame walk upwards (round 5; see the strip loop)
 constexpr bool kK3AltDir = true;
 // level nibbles of 4 cells from their key16 pairs (cells d, d + 1 | d + 2, d + 3): (k | 0x8000) - Q has
@@ -1063,7 +1068,7 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
       if (first) __syncthreads();
       if (first) {
         // levels: the mean key7 level of the first step's CUT rows (this thread's 16 cells), then the
-        // kK3LvQA / _QB quantiles of a 128-bin histogram around it
+        // kK3RulesQA / _QB quantiles of a 128-bin histogram around it
         float4 v[TR];
 #pragma unroll
         for (int u = 0; u < TR; ++u) v[u] = load_row(r0 + u);
@@ -1095,7 +1100,7 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
           int tot;
           const uint32_t ex = (uint32_t)wave_excl_scan((int)(c0 + c1), tot);
           const uint32_t cum0 = ex + c0, cum1 = ex + c0 + c1;
-          const uint32_t na = (uint32_t)(kK3LvQA * (TR * NC) / 1000), nb = (uint32_t)(kK3LvQB * (TR * NC) / 1000);
+          const uint32_t na = (uint32_t)(kK3RulesQA * (TR * NC) / 1000), nb = (uint32_t)(kK3RulesQB * (TR * NC) / 1000);
           const uint64_t ba0 = __ballot(cum0 >= na), ba1 = __ballot(cum1 >= na);
           const uint64_t bb0 = __ballot(cum0 >= nb), bb1 = __ballot(cum1 >= nb);
           auto first_bin = [](uint64_t m0, uint64_t m1) {
@@ -1110,7 +1115,9 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
         __syncthreads();
         const int h0u = __builtin_amdgcn_readfirstlane(h0);
         const uint32_t QA = (uint32_t)min(max((h0u + (int)__builtin_amdgcn_readfirstlane(cnt[14])) * 8, 1), 0x7f80);
-        const uint32_t QB = (uint32_t)min(max((h0u + (int)__builtin_amdgcn_readfirstlane(cnt[15])) * 8, 1), 0x7f80);
+        // B at most 1.5 A (key16 truncates: lo(key16(x)) <= x), at least A
+        const uint32_t QB = max(QA, min((uint32_t)min(max((h0u + (int)__builtin_amdgcn_readfirstlane(cnt[15])) * 8, 1), 0x7f80),
+                                        key16(1.5f * key_lo(QA))));
         // C / D one and two octaves above QB (exact: key16 + 128 doubles lo); the scale rules need them
         // inside the finite range and no scale override
         const bool s2ok = !a.override_ && QB + 256u < 0x7f80u;
