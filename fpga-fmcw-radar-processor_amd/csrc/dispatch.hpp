@@ -63,7 +63,6 @@ struct Cfar2Info {
   Cfar2DecideFn decide; // K3b k_cfar2d_decide
   Cfar2EmitFn emit;     // K3c k_cfar2d_emit
   size_t smem;          // K3a's dynamic LDS bytes
-  int decide_grid;      // K3b workgroups (more where K3a leaves more candidates: fmcw_api.hip)
 };
 Cfar2Info cfar2_info(uint32_t nc, int hd, int gd, int hr, int gr, bool compat);  // inst_cfar2.hip
 

@@ -565,9 +565,8 @@ constexpr size_t kCfar2Batch = 16;  // frames per 2-D CFAR launch on the caller'
 // After K3b's software pipeline (later in round 5; tools/k3_grid_ab.sh, profiles/r05/k3_grid/, two
 // interleaved passes, us per K3 batch, config 5 / config 3): 2048 / 1024 workgroups 261, 252 /
 // 75.6, 75.1; 1024 / 1024 258, 250 / 73.3, 72.3; 4096 / 1024 253, 255 / 81.7, 81.4; emit grids 256 /
-// 512 within noise.  In the bench's rocprof trace the config-5 decide took 22.2 us at 2048 and
-// 24.6 at 1024, config 3's 9.8 and 7.5: the grid follows the candidate count, 2048 workgroups
-// behind the rules kernel (Cfar2Info::decide_grid, ~10^5 candidates per launch), 1024 elsewhere.
+// 512 within noise.  With k_cfar2d_lv's later levels (8x fewer candidates at config 5) 2048 / 1024 /
+// 512 decide workgroups and emit grids 1024 / 256 all measured 222-231 us (k3grid2, noise): 1024.
 constexpr int kCfar2DecideGrid = 1024;
 constexpr int kCfar2EmitGrid = 1024;
 
@@ -860,10 +859,6 @@ int fmcw_create(const fmcw_config* cfg, fmcw_handle** out) {
     occupancy_grid(ci.fn, 256, h->cfar2d_smem, h->n_cu, &h->grid_cfar);
   }
   h->grid_k3b = kCfar2DecideGrid;
-  if (c.cfar_kind == FMCW_CFAR_OS2D) {
-    const Cfar2DArgs a = cfar2_args(c);
-    h->grid_k3b = cfar2_info(c.n_doppler, a.hd, a.gd, a.hr, a.gr, a.compat != 0).decide_grid;
-  }
   h->grid_k3c = kCfar2EmitGrid;
 #if FMCW_LAB
   // experiment knobs (tools/overlap_lab.py): cap a persistent grid so that another stream's

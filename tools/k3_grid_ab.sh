@@ -5,7 +5,7 @@ set -o pipefail
 cd ${GRAFT_REPO_ROOT:-/root/repo}
 O=${AB_OUT:-gpurun_out/k3grid}
 mkdir -p $O
-L=$PWD/fpga-fmcw-radar-processor_amd/lib/var_lab.so
+L=$PWD/fpga-fmcw-radar-processor_amd/lib/${LIB:-var_lab}.so
 for r in 1 2; do
   for g in ${GRIDS:-2048,1024 1024,1024 4096,1024 2048,256 2048,512}; do
     b=${g%,*}; c=${g#*,}
