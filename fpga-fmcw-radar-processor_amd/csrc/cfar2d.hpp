@@ -136,11 +136,11 @@ constexpr size_t cfar2d_smem_bytes(int hr) {
 // sliding row sums of those.  Every ref counted lies >= lo(Q), so fl(s_min r) >= P = fl(s_min lo(Q))
 // (rounding is monotone); a CUT with key16(cut) < U = key16(P) has cut < lo(U) <= P.  So
 // key16(cut) < U and count_Q >= need give E(s_min) >= need: the cell cannot detect at any scale
-// >= s_min.  Two levels A <= B per strip, at the kK3LvQA / _QB quantiles (56 % / 68 %) of
+// >= s_min.  Two levels A <= B per strip, at the kK3LvQA / _QB quantiles (50 % / 66 %) of
 // the key7 levels of the strip's first 4096 cells: a CUT is screened out if either level rules it
 // out.  Quantiles, not offsets from the mean, so the levels follow the clutter's spread (config 3's
 // 4-rx NCI cells are far narrower than config 5's Rayleigh ones).  Survivors on the bench maps
-// (tests' fixed seed, NumPy model of this screen): config 5 1.6 %, config 2 1.7 %, config 3
+// (tests' fixed seed, NumPy model of this screen, round 4's 56 % / 68 %): config 5 1.6 %, config 2 1.7 %, config 3
 // 0.014 % -- the round-3 pair screen 1.9 %, 2.0 %, 0.010 % -- at about a quarter of its VALU work.
 // Ring rows hold per cell one byte: bit 0 = key >= QA, bit 4 = key >= QB, so both levels' column
 // sums (<= 2 HR + 1 <= 15) add in the nibbles of one 32-bit add; the 13-cell row sums (<= 143) of
@@ -148,7 +148,10 @@ constexpr size_t cfar2d_smem_bytes(int hr) {
 // the two levels: quantiles (per mille) of the strip's first-step cells; rows of the level
 // screen's LDS reads in flight ahead of the accumulation (round 5: 2 or 3 measured alike, 2 keeps
 // k_cfar2d_lv spill-free at 4 waves per SIMD)
-constexpr int kK3LvQA = 560, kK3LvQB = 680, kK3ScreenAhead = 2;
+// (k_cfar2d: 50 % / 66 % since late round 5 -- NumPy model of the screen on config 3's map 0.014 % ->
+// 0.006 % survivors; config-3 K3 73.5-74.1 -> 68.2-69.2 us, lab, two passes; 52 / 66 70.9-71.4,
+// 50 / 64 69.6)
+constexpr int kK3LvQA = 500, kK3LvQB = 660, kK3ScreenAhead = 2;
 // k_cfar2d_lv's two levels (its scale rules change the optimum): the 50 % / 74 % quantiles, B clamped
 // to 1.5 A so that rule A stays available.  NumPy model of the rules on the config-5 bench map
 // (4 x 48 rows): survivors 0.0356 % at 56 / 68, 0.0041 % at 50 / 74; 48 / 76, where B passes 1.5 A
