@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--ns", type=int, default=1024)
     ap.add_argument("--nc", type=int, default=256)
     ap.add_argument("--variants", default="base,nocfar,nomap,bare,os2d,chunk16,chunk64,chunk128,mti2")
+    ap.add_argument("--spectrum", default="f32", help="f32 | f16 | s48 (the bench runs config 2 on s48)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -57,7 +58,7 @@ def main():
         v = variants[name]
         extra = {"cfar1d": v["cfar1d"]} if "cfar1d" in v else {}
         core = RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar=v["cfar"], max_frames=F, chunk_frames=v["chunk"],
-                         mti_bypass=not v["mti"], cfar_scale_ovr=v.get("ovr", 0), **extra)
+                         mti_bypass=not v["mti"], cfar_scale_ovr=v.get("ovr", 0), spectrum=a.spectrum, **extra)
 
         def step():
             core.enqueue(cube.data_ptr(), F, rd_map.data_ptr() if v["map"] else 0, dets.data_ptr(),
@@ -76,7 +77,7 @@ def main():
             step()
         kt = core.kernel_times()
         core.close()
-        out = {"variant": name, "frames_per_s": round(F / el), "ms_per_step": round(el * 1e3, 3),
+        out = {"variant": name, "spectrum": a.spectrum, "frames_per_s": round(F / el), "ms_per_step": round(el * 1e3, 3),
                "dets_per_frame": round(int(nd[0].item()) / F, 1)}
         for k, (ms, n) in kt.items():
             if n:
