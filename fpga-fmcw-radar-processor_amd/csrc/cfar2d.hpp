@@ -154,7 +154,7 @@ constexpr size_t cfar2d_smem_bytes(int hr) {
 constexpr int kK3LvQA = 500, kK3LvQB = 660, kK3ScreenAhead = 2;
 // k_cfar2d_lv's two levels (its scale rules change the optimum): the 50 % / 74 % quantiles, B clamped
 // to 1.5 A so that rule A stays available.  NumPy model of the rules on the config-5 bench map
-// (4 x 48 rows): survivors 0.0356 % at 56 / 68, 0.0041 % at 50 / 74; 48 / 76, where B passes 1.5 A
+// (tools/k3_rules_model.py, 4 x 48 rows): survivors 0.0356 % at 56 / 68, 0.0041 % at 50 / 74; 48 / 76, where B passes 1.5 A
 // unclamped, 2.2 %.
 constexpr int kK3RulesQA = 500, kK3RulesQB = 740;
 // k_cfar2d: odd strips of a frame walk upwards (round 5; see the strip loop)
@@ -799,9 +799,9 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
 //                                                <= 252 a   when b <= 1.5 a, C_A <= 80, C_B <= 40, C_C <= 8
 // (n = 128; C_A / C_B count refs, C_C / C_D the whole box), and the fp32 tree mean then stays below
 // 2 q (the tree sum of 128 non-negative terms is within 2^-21 of the sum).  RTL-compat cells: the
-// integer mean floor(sum / n) >> 1 is below the same bound.  NumPy model on the bench's maps
-// (tools/k3_screen_model.py --rules): survivors 1.60 % -> 0.033 % (config 5), 0.014 % -> 0.009 %
-// (config 3).
+// integer mean floor(sum / n) >> 1 is below the same bound.  NumPy model on the bench's maps (round
+// 5 at 56 % / 68 % levels): survivors 1.60 % -> 0.033 % (config 5), 0.014 % -> 0.009 % (config 3);
+// at the rules kernel's own levels (below) 0.004 % at config 5 (tools/k3_rules_model.py).
 //
 // LDS per ring row: two nibble PREFIX rows and a cut-code row (a nibble per cell: key16 < UA, UB, U2A,
 // U2B).  A prefix row holds per cell one byte of two 4-bit counters: nibble 0 = #{rows y of the strip
