@@ -85,3 +85,30 @@ def test_lv_compat():
     want = _rtl_dets(m, O.Cfar2D())
     assert len(want) > 0
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("dist", ["exponential", "lognormal", "uniform", "sparse"])
+def test_lv_clutter_shapes(dist):
+    """Clutter whose level spacing differs from the bench's Rayleigh magnitudes: exponential (power
+    maps: ~10 % of cells at the C level, so the C bound often fails), lognormal (wide: B clamped to
+    1.5 A), uniform (narrow), and a sparse map (mostly zeros: levels at the bottom of the key range).
+    The screen only ever keeps more cells; the detections must not change."""
+    rng = np.random.default_rng({"exponential": 81, "lognormal": 83, "uniform": 85, "sparse": 87}[dist])
+    shape = (2, NS, NC)
+    if dist == "exponential":
+        m = rng.exponential(5.0, shape)
+    elif dist == "lognormal":
+        m = rng.lognormal(1.0, 1.2, shape)
+    elif dist == "uniform":
+        m = rng.uniform(9.0, 11.0, shape)
+    else:
+        m = np.where(rng.random(shape) < 0.02, rng.rayleigh(10.0, shape), 0.0)
+    m = m.astype(np.float32)
+    m[0, 60, 100] = 4000.0
+    m[1, 200, 1020] = 3000.0
+    m[:, 120:124, 400:460] *= 30.0
+    with RadarCore(N_RANGE=NS, N_DOPPLER=NC, cfar="os2d", max_frames=2) as core:
+        got = run_cfar_stage(core, m, cap=1 << 21)
+    want = CB.cfar(m, O.Cfar2D(), threads=16)
+    assert len(want) >= 2
+    np.testing.assert_array_equal(got, want)
