@@ -149,6 +149,16 @@ SPECTRUM_FORMAT = {  # fmcw.h fmcw_spectrum_dtype; every arithmetic step is fp32
 }
 
 
+def shard_plan(world, rank, F):
+    """Frame sharding of one step (SURVEY.md 8e, weak scaling): every rank runs F frames of its
+    own, global frames [rank * F, (rank + 1) * F); its synthetic input is seeded by its first global
+    frame (seed 1234 + frame), and its detection records carry global frame ids
+    (frame_offset) on the wire, whose fixed message holds 128 records per frame."""
+    first = rank * F
+    return {"first_global": first, "seed": 1234 + first, "frames": F, "frame_offset": first,
+            "wire_cap": F * 128, "global_frames": world * F}
+
+
 def spectrum_of(wl, args, primary):
     """The corner-turned spectrum format a workload runs: --spectrum for the primary workload if
     given, else the workload's own (WORKLOADS)."""
@@ -173,8 +183,9 @@ def run_workload(name, args, world, rank, dev, primary, pmc, n_cu):
                      spectrum=spectrum_of(wl, args, primary))
     # synthetic input: 16 distinct frames (seed 1234 + global frame), tiled to F, resident in HBM
     n_u = min(16, F)
-    first_global = rank * F
-    u = synth.frames(n_u, ns, nc, nrx, wl["recipe"], seed=1234 + first_global, dtype=wl["dtype"])
+    plan = shard_plan(world, rank, F)
+    first_global = plan["first_global"]
+    u = synth.frames(n_u, ns, nc, nrx, wl["recipe"], seed=plan["seed"], dtype=wl["dtype"])
     if wl["dtype"] == "f32":
         u = u.view(np.float32)
     ut = torch.from_numpy(np.ascontiguousarray(u)).to(dev)
@@ -193,7 +204,8 @@ def run_workload(name, args, world, rank, dev, primary, pmc, n_cu):
     gather = primary and world > 1 and not args.no_gather
     gather_kind = None
     rg = None
-    wire_cap = F * 128                 # records per rank on the wire: 128 per frame (~64 found)
+    rccl_info = None
+    wire_cap = plan["wire_cap"]        # records per rank on the wire: 128 per frame (~64 found)
     use_rccl = args.gather == "rccl" and os.environ.get("FMCW_BENCH_BACKEND", "nccl") == "nccl"
     if gather and use_rccl:
         # libfmcw's fmcw_gather_dets: fixed-size ncclSend/ncclRecv to rank 0, device-side
@@ -203,6 +215,13 @@ def run_workload(name, args, world, rank, dev, primary, pmc, n_cu):
             dist.broadcast_object_list(obj, src=0)
             rg = RcclGather(obj[0], world, rank, local, wire_cap)
             gather_kind = "libfmcw fmcw_gather_dets (RCCL send/recv to rank 0, fixed wire_cap, no host sync)"
+            # what RCCL itself reports (fmcw_comm_info: ncclCommCount / UserRank / CuDevice), from
+            # every rank: the line then proves the gather spans `world` distinct GPUs
+            mine = rg.info()
+            infos = [None] * world
+            dist.all_gather_object(infos, mine)
+            rccl_info = {"rccl_ranks": mine["rccl_ranks"], "rccl_user_ranks": [i["rccl_rank"] for i in infos],
+                         "rccl_devices": [i["rccl_device"] for i in infos], "wire_cap": mine["wire_cap"]}
         except Exception as e:  # noqa: BLE001 -- reported, then the torch path is used
             print(f"rank {rank}: RCCL gather unavailable ({e}); using torch all_gather", file=sys.stderr)
             rg = None
@@ -370,10 +389,14 @@ def run_workload(name, args, world, rank, dev, primary, pmc, n_cu):
                                 "GBps_h2d": round(n_h * host.numel() * host.element_size() / th / 1e9, 1),
                                 "sample": f"{n_h} batches of {Fh} frames from pinned host memory, copy/compute overlapped"}
         del host, dbuf
+    if rccl_info is not None:
+        rec["config"]["rccl"] = rccl_info
+        rec["rccl_ranks"] = rccl_info["rccl_ranks"]
     if rg is not None and rank == 0:
         torch.cuda.synchronize(dev)
         rec["config"]["gathered_records_last_step"] = int(root_n[0].item())
         rec["config"]["gather_lost_last_step"] = int(root_n[1].item())
+        rec["gathered_records_last_step"] = int(root_n[0].item())
     core.close()
     if rg is not None:
         rg.close()
@@ -469,7 +492,8 @@ def main():
         "cpu_baseline": cpu,
     }
     for k in ("range_kernel", "chunk_frames", "detections_per_step", "status_words", "e2e_GBps_algorithmic",
-              "e2e_frac_of_peak", "kernels", "profiled_step_ms", "h2d_inclusive"):
+              "e2e_frac_of_peak", "kernels", "profiled_step_ms", "h2d_inclusive", "rccl_ranks",
+              "gathered_records_last_step"):
         if k in rec:
             out[k] = rec[k]
     out["h2d_inclusive_fps"] = rec.get("h2d_inclusive", {}).get("frames_per_s_per_gpu")

@@ -96,8 +96,11 @@ __global__ void __launch_bounds__(256) k_gather_compact(const fmcw_det* __restri
 // fmcw_comm_create's collective check: 3 words, all-reduced with max over the ranks (wire_cap,
 // ~wire_cap, any rank's allocation failure).  A static device array, so that no rank can fail to
 // obtain it and skip the collective its peers wait in.
+// One lock per device (the array has one instance per device): two ranks of one process on
+// different GPUs (a thread each) then never wait on each other's collective.
 __device__ uint64_t g_check[3];
-std::mutex g_check_mu;
+constexpr int kMaxCommDevices = 64;
+std::mutex g_check_mu[kMaxCommDevices];
 bool g_fail_next_alloc = false;  // fmcw_comm_fail_next_alloc_for_test
 
 // The verdict of the check, the same on every rank: the all-reduced words h (or this rank's own,
@@ -140,6 +143,7 @@ int fmcw_comm_create(const void* id, int n_ranks, int rank, int device_id, size_
   if (n_ranks < 1 || n_ranks > 64 || rank < 0 || rank >= n_ranks)
     return gfail(FMCW_EINVAL, "rank %d of %d (1..64 ranks)", rank, n_ranks);
   if (wire_cap < 1 || wire_cap > (1u << 26)) return gfail(FMCW_EINVAL, "wire_cap %zu (1..2^26)", wire_cap);
+  if (device_id < 0 || device_id >= kMaxCommDevices) return gfail(FMCW_EINVAL, "device_id %d (0..63)", device_id);
   if (hipSetDevice(device_id) != hipSuccess) {
     (void)hipGetLastError();
     return gfail(FMCW_ENODEV, "device_id %d", device_id);
@@ -172,7 +176,7 @@ int fmcw_comm_create(const void* id, int n_ranks, int rank, int device_id, size_
   if (n_ranks > 1) {
     // every rank must size its message alike (send / recv sizes match) and have its buffers: one
     // collective check here, the only host synchronisation of the communicator's life
-    std::lock_guard<std::mutex> lk(g_check_mu);  // one static check array per device and process
+    std::lock_guard<std::mutex> lk(g_check_mu[device_id]);  // this device's static check array
     void* v = nullptr;
     ncclResult_t rr = ncclSuccess;
     bool ok = hipGetSymbolAddress(&v, HIP_SYMBOL(g_check)) == hipSuccess;
@@ -216,6 +220,20 @@ int fmcw_comm_destroy(fmcw_comm* c) {
   if (c->wire) hipFree(c->wire);
   if (c->recv) hipFree(c->recv);
   delete c;
+  return FMCW_OK;
+}
+
+int fmcw_comm_info(const fmcw_comm* c, int* n_ranks, int* rank, int* device, size_t* wire_cap) {
+  if (!c || !c->comm) return gfail(FMCW_EINVAL, "null communicator");
+  int n = 0, r = 0, d = 0;
+  ncclResult_t e = ncclCommCount(c->comm, &n);
+  if (e == ncclSuccess) e = ncclCommUserRank(c->comm, &r);
+  if (e == ncclSuccess) e = ncclCommCuDevice(c->comm, &d);
+  if (e != ncclSuccess) return gfail(FMCW_EHIP, "RCCL communicator query: %s", ncclGetErrorString(e));
+  if (n_ranks) *n_ranks = n;
+  if (rank) *rank = r;
+  if (device) *device = d;
+  if (wire_cap) *wire_cap = c->wire_cap;
   return FMCW_OK;
 }
 

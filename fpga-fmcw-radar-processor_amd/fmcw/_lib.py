@@ -53,6 +53,7 @@ class FmcwConfig(C.Structure):
         ("cfar2d_scale_override", C.c_uint32),
         ("max_frames", C.c_uint32), ("chunk_frames", C.c_uint32), ("device_id", C.c_int32),
         ("compat_rtl", C.c_uint32), ("range_shift", C.c_uint32), ("spectrum_dtype", C.c_int32),
+        ("det_capacity", C.c_uint32),
     ]
 
 
@@ -99,6 +100,7 @@ SIGNATURES = {
     "fmcw_comm_unique_id": (_I, [_VP]),
     "fmcw_comm_create": (_I, [_VP, _I, _I, _I, _SZ, C.POINTER(_VP)]),
     "fmcw_comm_destroy": (_I, [_VP]),
+    "fmcw_comm_info": (_I, [_VP, C.POINTER(_I), C.POINTER(_I), C.POINTER(_I), C.POINTER(_SZ)]),
     "fmcw_gather_dets": (_I, [_VP, _VP, _SZ, _VP, C.c_uint32, _VP, _VP, _I, _VP]),
     "fmcw_comm_fail_next_alloc_for_test": (_I, [_I]),
     "fmcw_comm_check_decide_for_test": (_I, [C.POINTER(C.c_uint64), _I, _SZ]),

@@ -100,6 +100,13 @@ class RcclGather:
         L.check(L.load().fmcw_comm_unique_id(buf))
         return buf.raw
 
+    def info(self) -> dict:
+        """fmcw_comm_info: what RCCL reports for the communicator (ncclCommCount /
+        ncclCommUserRank / ncclCommCuDevice) and its wire_cap."""
+        n, r, d, w = C.c_int(), C.c_int(), C.c_int(), C.c_size_t()
+        L.check(self._lib.fmcw_comm_info(self._h, C.byref(n), C.byref(r), C.byref(d), C.byref(w)))
+        return {"rccl_ranks": n.value, "rccl_rank": r.value, "rccl_device": d.value, "wire_cap": w.value}
+
     def gather(self, dets_ptr: int, det_cap: int, n_dets_ptr: int, frame_offset: int,
                out_ptr: int | None, out_n_ptr: int | None, root: int = 0, stream: int = 0):
         """Device pointers; asynchronous on `stream`.  det_cap = the capacity of dets (as given to

@@ -152,7 +152,8 @@ class RadarCore:
                  cfar1d=(8, 2, 12, 4.0), in_dtype: str = "f32", window: str = "hamming",
                  magnitude: str = "abs", map_kind: str = "linear", max_frames: int = 1,
                  chunk_frames: int = 0, device: int = 0, mti_bypass: bool = True,
-                 NOTCH_MODE: int = 2, compat_rtl=(), range_shift: int = 0, spectrum: str = "f32"):
+                 NOTCH_MODE: int = 2, compat_rtl=(), range_shift: int = 0, spectrum: str = "f32",
+                 det_capacity: int = 0):
         """mti_bypass / NOTCH_MODE mirror radar_core's u_mti (radar_core.vhd:329-338, port
         :48).  The RTL port defaults to '0' (MTI on); this mirror defaults to bypass because
         the north-star path and BASELINE configs exclude MTI and tb_radar_core bypasses it
@@ -163,10 +164,14 @@ class RadarCore:
         doppler_notch.vhd:73-93).  range_shift: range spectrum scaled by 2^-range_shift (the
         FFT IP's fixed scaling schedule), so that the 16-bit spectrum words of the compat MTI and
         of window="q15_rtl" (integer windows on both axes) are meaningful.
-        spectrum: "f32" or "f16", the element type of the internal corner-turned spectrum
-        (fmcw.h fmcw_spectrum_dtype: "f16" halves its HBM traffic, map within 2e-3; "s48" takes 6
-        bytes per point -- a 23-bit significand per component, one exponent per 4 chirps -- map
-        within the 1e-4 of "f32"; n_range <= 1024, n_doppler >= 64, MTI off)."""
+        spectrum: "f32", "f16" or "s48", the element type of the internal corner-turned spectrum
+        (fmcw.h fmcw_spectrum_dtype): "f16" halves its HBM traffic, map within 2e-3; "s48" takes 6
+        bytes per point, map within the 1e-4 of "f32" -- a chirp group of a range bin shares one
+        8-bit exponent: quads of 23-bit significands at n_range <= 1024 (adjacent chirps up to
+        n_range 512, chirps n_doppler / 16 apart at 1024), pairs of 22-bit significands n_doppler /
+        16 apart above; needs n_doppler >= 64 and MTI off.
+        det_capacity: detection records one call can hold (fmcw.h fmcw_config.det_capacity); 0 =
+        every cell of max_frames frames, so no call loses a detection its det_cap has room for."""
         lib = L.load()
         cfg = L.default_config()
         cfg.mti_mode = L.MTI_OFF if mti_bypass else {2: L.MTI_2PULSE, 3: L.MTI_3PULSE}[NOTCH_MODE]
@@ -189,6 +194,7 @@ class RadarCore:
             sum(flags[k] for k in set(compat_rtl))
         cfg.range_shift = range_shift
         cfg.spectrum_dtype = {"f32": L.SPEC_F32, "f16": L.SPEC_F16, "s48": L.SPEC_S48}[spectrum]
+        cfg.det_capacity = det_capacity
         self.cfg = cfg
         self.in_dtype = in_dtype
         self.device = device

@@ -61,7 +61,7 @@
 extern "C" {
 #endif
 
-#define FMCW_ABI_VERSION 7  /* 2: fmcw_config grew compat_rtl, range_shift (27 words, 108 B);
+#define FMCW_ABI_VERSION 8  /* 2: fmcw_config grew compat_rtl, range_shift (27 words, 108 B);
                                3: + spectrum_dtype (28 words, 112 B);
                                4: FMCW_K_COUNT 5 -> 6, FMCW_INFO_PAIR_CHUNK;
                                5: n_dets_dev holds FMCW_STATUS_WORDS (4) words (saturation
@@ -74,7 +74,10 @@ extern "C" {
                                   environment variable;
                                7: fmcw_enqueue / fmcw_cfar graph-capturable (device-resident
                                   ordering tag); fmcw_comm_fail_next_alloc_for_test,
-                                  fmcw_comm_check_decide_for_test; FMCW_SPEC_S48 */
+                                  fmcw_comm_check_decide_for_test; FMCW_SPEC_S48;
+                               8: fmcw_config grew det_capacity (29 words, 116 B): the detection
+                                  scratch holds every cell by default, so a call loses no detection
+                                  its det_cap has room for; fmcw_comm_info */
 
 typedef enum {
   FMCW_OK = 0,
@@ -138,11 +141,11 @@ typedef struct fmcw_config {
   uint32_t chunk_frames;   /* frames per internal kernel chunk (0 = auto: a chunk's corner-turned
                             * spectrum within 208 MiB of the 256 MiB Infinity Cache, no rounding;
                             * 104 frames at 1024 x 256 fp32, 3 at 4096 x 512 x 4 rx or 8192 x 1024).
-                            * Device memory of a handle: the chunk's spectrum (8 B per point), a
-                            * detection scratch of ~1/32 + 1/64 of max_frames' cells (16 B each),
-                            * and with the 2-D CFAR a chunk-sized linear map (4 B per cell) and
-                            * candidate lists of 8 B per cell for min(max_frames, 16 + chunk,
-                            * 2^32 cells) frames -- 1.2 GiB at 8192 x 1024 with the auto chunk */
+                            * Device memory of a handle: the chunk's spectrum (8 B per point), the
+                            * detection scratch (det_capacity below: 16 B per record), and with the
+                            * 2-D CFAR a chunk-sized linear map (4 B per cell) and candidate lists of
+                            * 8 B per cell for min(max_frames, 16 + chunk, 2^32 cells) frames --
+                            * 1.2 GiB at 8192 x 1024 with the auto chunk */
   int32_t device_id;       /* HIP device ordinal */
   /* RTL-compat arithmetic, a bitmask of fmcw_compat; 0 = the fp32 build spec */
   uint32_t compat_rtl;
@@ -152,6 +155,16 @@ typedef struct fmcw_config {
   uint32_t range_shift;
   /* fmcw_spectrum_dtype: element type of the internal corner-turned spectrum */
   int32_t spectrum_dtype;
+  /* Detection records the handle's scratch holds for one call beyond each wave tile's own slot
+   * (1/32 of its cells; a denser tile moves its whole run to this shared region).
+   * 0 (default) = every cell of max_frames frames (16 B per cell: 4 GiB at 1024 frames of
+   * 1024 x 256): no call can lose a detection, at any density the CFAR parameters produce -- the
+   * reference emits every non-zero CFAR output (radar_core.vhd:413-418), and cfar_scale_ovr = 1 or
+   * a 1-D alpha of 1 detect ~25 % of noise cells.  N > 0 bounds it to N records, for callers
+   * that bound det_cap: a call then loses records (status word [1]) only when it finds more than
+   * N detections, i.e. never while det_cap <= N would have room for the whole list.
+   * max_frames x cells (+ slots) must stay below 2^32 records. */
+  uint32_t det_capacity;
 } fmcw_config;
 
 /* fmcw_config.spectrum_dtype.  FMCW_SPEC_F16 stores the corner-turned spectrum (K1 -> K2) as
@@ -162,8 +175,8 @@ typedef struct fmcw_config {
  * Not with FMCW_COMPAT_MTI (its 16-bit words are defined on the fp32 spectrum).
  * FMCW_SPEC_S48 stores it in 6 bytes per point (config 2: 2 -> 1.5 MiB written and read back per
  * frame; configs 3 / 5: 64 -> 48 MiB, so the auto chunk holds 4 frames instead of 3): a group of
- * G chirps of a range bin (n_doppler / 16 apart at n_range = 1024, else adjacent) shares one 8-bit
- * exponent E (the largest of their 2G components is
+ * G chirps of a range bin (adjacent quads at n_range <= 512; chirps n_doppler / 16 apart at
+ * n_range = 1024 (quads) and above (pairs)) shares one 8-bit exponent E (the largest of their 2G components is
  * < 2^E), and every component is a W-bit signed significand of 2^(E - W + 1), i.e. exact to 2^-W
  * of the group's largest component (fp32: 2^-24 of each) -- G = 4, W = 23 at n_range <= 1024;
  * G = 2, W = 22 above.  The map stays within the 1e-4 tolerance of FMCW_SPEC_F32 (per frame and
@@ -246,11 +259,11 @@ int fmcw_destroy(fmcw_handle* h);
  * left them as the previous call wrote them); it may be NULL only when cfar_kind == NONE (then
  * no status):
  *   [0] detections found (may exceed det_cap; entries beyond det_cap are not written),
- *   [1] detections lost because the handle's internal detection scratch overflowed (a tile
- *       with more than its slot that also found the shared overflow region full).  Non-zero
- *       means the list is incomplete; fmcw_process returns FMCW_EDETCAP then.  0xffffffff:
- *       the ordering pass could not complete (a safety net that bounds its wait; not expected),
- *       the whole list is void,
+ *   [1] detections lost because the handle's detection scratch overflowed: only possible with
+ *       cfg.det_capacity = N > 0 and more than N detections found (the default scratch holds
+ *       every cell).  Non-zero means the list is incomplete; fmcw_process returns FMCW_EDETCAP
+ *       then.  0xffffffff: the ordering pass could not complete (a safety net that bounds its
+ *       wait; not expected), the whole list is void,
  *   [2] samples saturated by the RTL-compat integer windows (FMCW_WIN_Q15_RTL, either axis;
  *       win1 / win2 saturation_flag, window_multiplier.vhd:152-158),
  *   [3] samples whose int16 spectrum word or canceller output was clipped (FMCW_COMPAT_MTI or
@@ -292,6 +305,10 @@ int fmcw_comm_unique_id(void* id_out);
 int fmcw_comm_create(const void* id, int n_ranks, int rank, int device_id, size_t wire_cap,
                      fmcw_comm** out);
 int fmcw_comm_destroy(fmcw_comm* c);
+/* What RCCL itself reports for the communicator (ncclCommCount / ncclCommUserRank /
+ * ncclCommCuDevice), so that a multi-GPU run can show the collective really spans n_ranks GPUs;
+ * wire_cap as created.  Any output pointer may be NULL. */
+int fmcw_comm_info(const fmcw_comm* c, int* n_ranks, int* rank, int* device, size_t* wire_cap);
 int fmcw_gather_dets(fmcw_comm* c, const fmcw_det* dets_dev, size_t det_cap,
                      const uint32_t* n_dets_dev, uint32_t frame_offset, fmcw_det* out_dev,
                      uint32_t* out_n_dev, int root, void* stream);

@@ -38,7 +38,7 @@ def test_header_enums_match_binding():
     assert enum["FMCW_INFO_WORD_SATURATIONS"] == L.INFO_WORD_SATURATIONS
     assert enum["FMCW_INFO_CFAR2D_STEPS"] == L.INFO_CFAR2D_STEPS
     assert enum["FMCW_PARAM_CFAR2D_STEPS"] == L.PARAM_CFAR2D_STEPS
-    assert re.search(r"#define FMCW_ABI_VERSION 7\b", src)
+    assert re.search(r"#define FMCW_ABI_VERSION 8\b", src)
     assert int(re.search(r"#define FMCW_STATUS_WORDS (\d+)", src).group(1)) == L.STATUS_WORDS
 
 
@@ -93,7 +93,8 @@ def test_no_wide_store_data_hazard(lib_built, tmp_path):
 
 def test_struct_layouts():
     assert C.sizeof(L.FmcwDet) == 16
-    assert C.sizeof(L.FmcwConfig) == 28 * 4          # ABI 3-7 (fmcw.h FMCW_ABI_VERSION)
+    assert C.sizeof(L.FmcwConfig) == 29 * 4          # ABI 8 (fmcw.h FMCW_ABI_VERSION): + det_capacity
+    assert L.FmcwConfig.det_capacity.offset == 28 * 4
     assert L.FmcwDet.range.offset == 4 and L.FmcwDet.mag.offset == 8
 
 
@@ -107,8 +108,9 @@ def test_defaults_mirror_radar_core(lib_built):
             cfg.cfar2d_scale_max, cfg.cfar2d_scale_override) == (75, 2, 4, 6, 0)
     assert (cfg.cfar1d_ref, cfg.cfar1d_guard, cfg.cfar1d_rank) == (8, 2, 12)
     assert cfg.cfar1d_alpha == 4.0
-    assert lib_built.fmcw_abi_version() == 7
+    assert lib_built.fmcw_abi_version() == 8
     assert (cfg.compat_rtl, cfg.range_shift, cfg.spectrum_dtype) == (0, 0, L.SPEC_F32)
+    assert cfg.det_capacity == 0    # the detection scratch holds every cell: nothing is ever lost
     assert b"gfx950" in lib_built.fmcw_version()
 
 
@@ -200,6 +202,11 @@ def test_gather_argument_checks(lib_built):
     assert lib_built.fmcw_gather_pack_for_test(None, 1, None, 1, 0, None, None) == L.FMCW_EINVAL
     assert lib_built.fmcw_gather_compact_for_test(None, 65, 1, None, None, None) == L.FMCW_EINVAL
     assert lib_built.fmcw_comm_destroy(None) == L.FMCW_OK
+    n = C.c_int(-1)
+    assert lib_built.fmcw_comm_info(None, C.byref(n), None, None, None) == L.FMCW_EINVAL
+    assert b"communicator" in lib_built.fmcw_last_error() and n.value == -1
+    assert lib_built.fmcw_comm_create(idbuf, 1, 0, 64, 16, C.byref(h)) == L.FMCW_EINVAL   # device 0..63
+    assert b"device_id" in lib_built.fmcw_last_error()
 
 
 def test_integration_doc_struct_sizes():

@@ -222,3 +222,50 @@ def test_comm_create_failure_fails_every_rank(fail_rank, caps, want):
         assert rc == code, (rank, rc, msg)
         if want == "ENOMEM":
             assert ("per rank" in msg) == (rank == fail_rank) and (("another rank" in msg) == (rank != fail_rank))
+
+
+def _worker_bench_plan(rank, world, port, F, q):
+    """bench.py's per-rank shard plan (bench.shard_plan, used by run_workload) at world size 2:
+    first global frame rank * F, seed 1234 + that frame, and the detection gather with its
+    frame_offset yields global frames 0 .. world * F - 1 in order (config 4's frame sharding)."""
+    import sys
+    from conftest import REPO
+    if str(REPO) not in sys.path:
+        sys.path.insert(0, str(REPO))
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        plan = bench.shard_plan(world, rank, F)
+        plans = [None] * world
+        dist.all_gather_object(plans, plan)
+        # two detections per local frame (local frame ids, as fmcw_enqueue writes them)
+        rec = torch.zeros((2 * F, 4), dtype=torch.int32)
+        rec[:, 0] = torch.arange(2 * F) // 2
+        rec[:, 1] = (torch.arange(2 * F) % 2) * 100 + 7
+        allr, counts = gather_detections(rec, 2 * F, frame_offset=plan["frame_offset"])
+        q.put((rank, plans, counts, allr[:, 0].tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_shard_plan_gloo():
+    """Round-5 verdict item 5: the bench's per-rank frame offsets, over gloo at world size 2."""
+    world, F = 2, 1024
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_bench_plan, args=(r, world, port, F, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, plans, counts, frames in res:
+        assert [p["first_global"] for p in plans] == [0, F]
+        assert [p["seed"] for p in plans] == [1234, 1234 + F]
+        assert all(p["wire_cap"] == 128 * F and p["global_frames"] == world * F for p in plans)
+        assert counts == [2 * F, 2 * F]
+        assert frames == sorted(frames) and frames[0] == 0 and frames[-1] == world * F - 1
+        assert frames == [f // 2 for f in range(2 * world * F)]
