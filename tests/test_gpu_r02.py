@@ -149,18 +149,26 @@ def test_cfar2d_dense_tiles_use_overflow_region():
     np.testing.assert_array_equal(got, want)
 
 
-def test_dropped_detections_are_reported():
-    """Detections beyond the handle's scratch (slots + overflow region) are counted in
-    n_dets[1] and make fmcw_process return FMCW_EDETCAP, never silently lost."""
+@pytest.mark.parametrize("det_capacity", [0, 65536])
+def test_dropped_detections_are_reported(det_capacity):
+    """A map on which 255 of every 256 cells detect.  With the default scratch (ABI 8: every
+    cell) the whole list is stored and exact; with a bounded one (det_capacity = 65536 overflow
+    records) the detections beyond it are counted in n_dets[1] (fmcw_process: FMCW_EDETCAP),
+    never silently lost."""
     ns, nc = 1024, 256
     ramp = np.broadcast_to(np.arange(1, nc + 1, dtype=np.float32), (1, ns, nc)).copy()
-    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os1d", cfar1d=(1, 0, 0, 1.0), max_frames=1) as core:
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os1d", cfar1d=(1, 0, 0, 1.0), max_frames=1,
+                   det_capacity=det_capacity) as core:
         got, n, dropped = _stage_dets(core, ramp, cap=1 << 19)
         want = oracle_dets(ramp, O.Cfar1D(ref=1, guard=0, rank=0, alpha=1.0))
-        # every detection is counted; those beyond the scratch (8192 slot + 65536 overflow
-        # entries at max_frames 1) are reported as dropped
         assert n == len(want) == ns * (nc - 1)
-        assert dropped >= n - (8192 + 65536)
+        if det_capacity:
+            # every detection is counted; those beyond the scratch (8192 slot + 65536 overflow
+            # entries at max_frames 1) are reported as dropped
+            assert dropped >= n - (8192 + det_capacity)
+        else:
+            assert dropped == 0
+            np.testing.assert_array_equal(got, want)
         # the same map well inside the scratch is complete and exact
         small = ramp[:, :64].copy()
         got2, n2, dropped2 = _stage_dets(core, np.concatenate([small, np.zeros((1, ns - 64, nc), np.float32)], 1))
