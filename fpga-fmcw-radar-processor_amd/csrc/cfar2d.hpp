@@ -43,6 +43,10 @@ struct Cfar2Cands {
   float* thr;
   uint32_t* tiles;
   uint32_t* ctr;
+  // k_cfar2d_lv's strip-private spill regions (room for every cell / wave tile of the launch: a
+  // strip's part starts at its first cell / wave tile), copied into cell / tiles at the strip's end
+  uint32_t* pcell;
+  uint32_t* ptile;   // 2 words per wave tile
 };
 
 // 7-bit keys.  key(v) = clamp((bits(v) >> SH) - base, 0, 127) for a non-negative fp32 cell v:
@@ -61,7 +65,8 @@ __device__ __forceinline__ uint32_t key7(float v, int base) {
 }
 // key(q) + 1 for q = fl(c * inv_s) + 8 ulps (c * fl(1 / s): <= 2 ulps of error), c = the CUT:
 // a pair max whose key is >= this has max > q > c / s in reals, so fl(s * max) >= c.
-// (No NaN test: a NaN cut gets 128, which no key reaches, so the cell is never screened out.)
+// (No NaN test: a NaN cut gets 128, which no key reaches, so this round-3 screen never screens it
+// out; the level screens do -- NaN cells are outside the specification, fmcw.h fmcw_cfar.)
 __device__ __forceinline__ uint32_t cut_key7(float c, float inv_s, int base) {
   const int k = (int)((__float_as_uint(c * inv_s) + 8u) >> kK3KeyShift) - base;
   return (uint32_t)min(max(k, 0), 127) + 1u;
@@ -857,7 +862,7 @@ __device__ __forceinline__ uint32_t lv_cut_code(uint2 kw, const uint32_t (&W)[4]
 template <int HR, int GR>
 __device__ __forceinline__ uint32_t cfar2d_screen_prefix(const uint8_t* hiA, const uint8_t* loA, const uint8_t* hiC,
                                                          const uint8_t* loC, const uint8_t* hiG, const uint8_t* loG,
-                                                         uint2 cw, int need, bool ruleA) {
+                                                         uint2 cw, int need, bool ruleA, bool zaware) {
   static_assert((2 * HR + 1) * 13 - (2 * GR + 1) * 5 == 128 && 2 * HR + 1 <= 15 && 5 * (2 * GR + 1) <= 15,
                 "thresholds below are for n_ref 128");
   uint32_t V[8], G[6], W[8];
@@ -944,6 +949,10 @@ __device__ __forceinline__ uint32_t cfar2d_screen_prefix(const uint8_t* hiA, con
     const uint32_t rB = nb2 & ~(CB + K(64)) & okC32[m] & okD & (nb << 4);   // C_B <= 63, C_C <= 32
     const uint32_t rA = na & ~(CA + K(47)) & ~(CB + K(87)) & okC8[m] & okA & (nb << 5);  // 80, 40, 8
     sv[m] = ~(smin | rA | rB) & H;
+    if (zaware) {  // uniform: code 0x1 (no key16 gives it) marks a +0 CUT, which never detects
+      const uint32_t x = nb ^ 0x01010101u;        // bytes <= 0x0F: + 0x7F sets bit 7 iff the byte is not 0
+      sv[m] &= (x + 0x7F7F7F7Fu);
+    }
   }
   // the survivor bits in cell order, only where there are any (a few lanes in a thousand)
   uint32_t bits = 0;
@@ -975,34 +984,67 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
   extern __shared__ __attribute__((aligned(16))) uint8_t smem8[];
   uint8_t* const ring = smem8;
   uint32_t* const hist = reinterpret_cast<uint32_t*>(ring + NR * ROWB);
-  uint32_t* const cnt = hist + 128;    // [0..3] wave counts, [4] / [5] buffer fill, [6] / [7] flush bases
+  uint32_t* const cnt = hist + 128;    // [0..3] wave counts, [4] / [5] buffer fill, [6] / [7] list bases,
+                                       // [8] / [9] private-region fill
   uint32_t* const buf = cnt + 16;      // the strip's survivor cells (Gm::CAPB)
   uint32_t* const bt = buf + Gm::CAPB; // their wave tiles: (tile, offset << 16 | count) (Gm::CAPT)
   constexpr int CAPB = Gm::CAPB, CAPT = Gm::CAPT;
-  // The candidate list takes a strip's survivors in one reservation (two atomics per flush): an
-  // atomic per wave tile on the launch's two counters -- every workgroup on the same two words --
-  // cost ~0.5 ms per launch with ~10^5 survivors (config 5, measured).
-  auto flush = [&]() {  // uniform; every thread of the workgroup calls it
-    const uint32_t n = cnt[4], m = cnt[5];
+  // The candidate list takes a strip's survivors in ONE reservation at the strip's end (two atomics):
+  // an atomic per wave tile on the launch's two counters -- every workgroup on the same two words --
+  // cost ~0.5 ms per launch with ~10^5 survivors (config 5, measured), and round 5's flush of a full
+  // LDS buffer (two atomics per flush) and its dense steps (two per wave tile) serialised on those
+  // words at 3.0 ms per 16-frame launch on heavy-tailed clutter (round 6, tools/cfar2d_bench.py
+  // --maps).  Survivors collect in the LDS buffer (a few per step on radar maps); a full buffer, and a
+  // step with more survivors than it holds, go to the strip's PRIVATE region of cands.pcell / .ptile
+  // (room for every cell and wave tile of the strip: no atomic), which the strip's end copies behind
+  // the buffer's remainder.  pcell / ptile hold (cell) and (rel tile | count << 16, run offset).
+  auto spill = [&](uint32_t pc0, uint32_t pt0) {  // uniform: the LDS buffer -> the private region
+    const uint32_t n = cnt[4], m = cnt[5], pn = cnt[8], pm = cnt[9];
     if (n == 0u) return;
-    __syncthreads();  // every thread has read cnt[4], cnt[5]
+    for (uint32_t i = threadIdx.x; i < n; i += NT) cands.pcell[pc0 + pn + i] = buf[i];
+    for (uint32_t j = threadIdx.x; j < m; j += NT) {
+      const uint32_t oc = bt[2 * j + 1];
+      cands.ptile[2 * (pt0 + pm + j)] = (bt[2 * j] - (uint32_t)tile0 - pt0) | ((oc & 0xffffu) << 16);
+      cands.ptile[2 * (pt0 + pm + j) + 1] = pn + (oc >> 16);
+    }
+    __syncthreads();  // every thread has read cnt and the buffer
     if (threadIdx.x == 0) {
-      cnt[6] = atomicAdd(&cands.ctr[0], n);
-      cnt[7] = atomicAdd(&cands.ctr[1], m);
+      cnt[8] = pn + n;
+      cnt[9] = pm + m;
       cnt[4] = cnt[5] = 0u;
     }
     __syncthreads();
+  };
+  auto finish = [&](uint32_t pc0, uint32_t pt0) {  // uniform; the strip's end
+    const uint32_t n = cnt[4], m = cnt[5], pn = cnt[8], pm = cnt[9];
+    if (n + pn == 0u) return;
+    __syncthreads();  // every thread has read cnt[4], [5], [8], [9]
+    if (threadIdx.x == 0) {
+      cnt[6] = atomicAdd(&cands.ctr[0], n + pn);
+      cnt[7] = atomicAdd(&cands.ctr[1], m + pm);
+      cnt[4] = cnt[5] = cnt[8] = cnt[9] = 0u;
+    }
+    __syncthreads();
     const uint32_t p0 = cnt[6], q0 = cnt[7];
-    for (uint32_t i = threadIdx.x; i < n; i += NT) cands.cell[p0 + i] = buf[i];
+    // the private region first (written by this workgroup's waves before the barriers above)
+    for (uint32_t i = threadIdx.x; i < pn; i += NT) cands.cell[p0 + i] = cands.pcell[pc0 + i];
+    for (uint32_t i = threadIdx.x; i < n; i += NT) cands.cell[p0 + pn + i] = buf[i];
+    for (uint32_t j = threadIdx.x; j < pm; j += NT) {
+      const uint32_t w0 = cands.ptile[2 * (pt0 + j)], off = cands.ptile[2 * (pt0 + j) + 1];
+      const uint32_t wt = (uint32_t)tile0 + pt0 + (w0 & 0xffffu);
+      cands.tiles[q0 + j] = wt;
+      sink.wg_base[wt] = p0 + off;
+      sink.wg_count[wt] = w0 >> 16;
+    }
     for (uint32_t j = threadIdx.x; j < m; j += NT) {
       const uint32_t wt = bt[2 * j], oc = bt[2 * j + 1];
-      cands.tiles[q0 + j] = wt;
-      sink.wg_base[wt] = p0 + (oc >> 16);
+      cands.tiles[q0 + pm + j] = wt;
+      sink.wg_base[wt] = p0 + pn + (oc >> 16);
       sink.wg_count[wt] = oc & 0xffffu;
     }
     __syncthreads();  // the buffer is free again
   };
-  if (threadIdx.x == 0) cnt[4] = cnt[5] = 0u;
+  if (threadIdx.x == 0) cnt[4] = cnt[5] = cnt[8] = cnt[9] = 0u;
 
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1019,11 +1061,19 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
   uint32_t qa2 = 0, qb2 = 0, qc2 = 0, qd2 = 0;
   uint32_t Wc[4] = {0, 0, 0, 0};
   bool ruleA = false;
+  // zero-aware strip (most of its first step's cells are +0 or tiny: a sparse or blank map): the cut
+  // code of a +0 CUT becomes 0x1, which the screen rules out -- E(s) counts every reference of a +0
+  // CUT (refs >= +0), so it cannot detect.  Without it every +0 cell of such a strip survived the
+  // level rules (its refs are mostly below every level) and K3b decided all of them: 26.8 ms per
+  // 16-frame launch on a map with 98 % zeros (round 6, tools/cfar2d_bench.py --maps sparse).
+  bool zaware = false;
   uint32_t pab = 0, pcd = 0;  // this column's running prefixes (A / B, C / D)
   // one ring slot's cells dt .. dt + 3: level bits into the prefixes, prefixes and cut codes to LDS
   auto stage = [&](int slot, float4 v) {
     if constexpr (CMP) v = q17x4(v);
-    // key16 without the NaN / negative cells (-> 0): a sign or NaN bit pattern is above inf's
+    // key16 without the NaN / negative cells (-> 0): a sign or NaN bit pattern is above inf's.  The
+    // cut codes use the same keys, so a NaN CUT is screened out: NaN cells are outside the
+    // specification (fmcw.h, fmcw_cfar), where the sorting and the counting OS-CFAR disagree
     const uint32_t b0 = __float_as_uint(v.x), b1 = __float_as_uint(v.y), b2 = __float_as_uint(v.z),
                    b3 = __float_as_uint(v.w);
     const uint32_t s0 = b0 <= 0x7f800000u ? b0 : 0u, s1 = b1 <= 0x7f800000u ? b1 : 0u;
@@ -1042,7 +1092,13 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
       *reinterpret_cast<uint32_t*>(rp + pidx(dt - NC)) = pab;
       *reinterpret_cast<uint32_t*>(rp + RB + pidx(dt - NC)) = pcd;
     }
-    *reinterpret_cast<uint16_t*>(rp + 2 * RB + dt / 2) = (uint16_t)lv_cut_code(kw, Wc);
+    uint32_t code = lv_cut_code(kw, Wc);
+    if (zaware) {  // uniform: +0 cells (s == 0 after the sanitising) get code 0x1
+      const uint32_t z = (s0 == 0u ? 0x000Fu : 0u) | (s1 == 0u ? 0x00F0u : 0u) | (s2 == 0u ? 0x0F00u : 0u) |
+                         (s3 == 0u ? 0xF000u : 0u);
+      code = (code & ~z) | (z & 0x1111u);
+    }
+    *reinterpret_cast<uint16_t*>(rp + 2 * RB + dt / 2) = (uint16_t)code;
   };
 
   for (int g = blockIdx.x; g < n_strips; g += gridDim.x) {
@@ -1058,6 +1114,9 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
     int base = 0;  // ring slot of tile row 0
     float4 pre[TR];
     const bool up = kK3AltDir && ((g / nf) & 1);  // odd strips walk upwards, as k_cfar2d's
+    // the strip's private region: its first cell and first wave tile in the launch
+    const uint32_t pc0 = ((uint32_t)f * (uint32_t)ns + (uint32_t)(t_beg * TR)) * (uint32_t)NC;
+    const uint32_t pt0 = (uint32_t)(f * wt_per_frame + t_beg * WPB);
     const int xo = up ? 0 : 1;
     for (int k = 0; k < t_end - t_beg; ++k) {
       const int t = up ? t_end - 1 - k : t_beg + k;
@@ -1133,6 +1192,7 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
         const uint32_t UA = key16(a.s_min * key_lo(QA)), UB = key16(a.s_min * key_lo(QB));
         const uint32_t U2A = s2ok ? key16(s2 * key_lo(QA)) : 0u, U2B = s2ok ? key16(s2 * key_lo(QB)) : 0u;
         ruleA = s2ok && key_lo(QB) <= 1.5f * key_lo(QA);
+        zaware = QA < 16u;  // the 50 % quantile level below 2^-124: at least half the cells are ~zero
         const uint32_t U[4] = {UA, UB, U2A, U2B};
 #pragma unroll
         for (int k2 = 0; k2 < 4; ++k2) Wc[k2] = ((U[k2] | 0x8000u) - 1u) * 0x00010001u;
@@ -1185,7 +1245,7 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
         const uint8_t* const lA = up ? p_hi : p_lo;
         const uint8_t* const hG = up ? g_lo : g_hi;
         const uint8_t* const lG = up ? g_hi : g_lo;
-        surv = cfar2d_screen_prefix<HR, GR>(hA, lA, hA + RB, lA + RB, hG, lG, cw, need, ruleA);
+        surv = cfar2d_screen_prefix<HR, GR>(hA, lA, hA + RB, lA + RB, hG, lG, cw, need, ruleA, zaware);
       }
       // emission: each wave tile's survivors, in (range, doppler) order, as one run of the strip
       // buffer (flushed to the candidate list when full and at the strip's end); an empty tile is
@@ -1209,21 +1269,18 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
         nt += c ? 1u : 0u;
       }
       if (T != 0u) {  // uniform
-        if (cnt[4] + T > (uint32_t)CAPB || cnt[5] + nt > (uint32_t)CAPT) flush();
+        if (cnt[4] + T > (uint32_t)CAPB || cnt[5] + nt > (uint32_t)CAPT) spill(pc0, pt0);
         const uint32_t bn = cnt[4], tn = cnt[5];
         const uint32_t cbase = ((uint32_t)f * (uint32_t)ns + (uint32_t)r) * (uint32_t)NC + (uint32_t)d0;
-        if (T > (uint32_t)CAPB) {  // a dense step: its own reservation, one per wave tile
+        if (T > (uint32_t)CAPB) {  // a dense step: straight into the private region (the buffer is empty)
           if (k_w) {
-            uint32_t p0 = 0u;
+            const uint32_t pn = cnt[8] + woff, pm = cnt[9] + ti;
             if (lane == 0) {
-              p0 = atomicAdd(&cands.ctr[0], (uint32_t)k_w);
-              cands.tiles[atomicAdd(&cands.ctr[1], 1u)] = (uint32_t)wtile;
-              sink.wg_base[wtile] = p0;
-              sink.wg_count[wtile] = (uint32_t)k_w;
+              cands.ptile[2 * (pt0 + pm)] = ((uint32_t)wtile - (uint32_t)tile0 - pt0) | ((uint32_t)k_w << 16);
+              cands.ptile[2 * (pt0 + pm) + 1] = pn;
             }
-            p0 = (uint32_t)__shfl((int)p0, 0, 64);
-            uint32_t o = p0 + (uint32_t)ex;
-            for (uint32_t m = surv; m; m &= m - 1, ++o) cands.cell[o] = cbase + (uint32_t)__builtin_ctz(m);
+            uint32_t o = pc0 + pn + (uint32_t)ex;
+            for (uint32_t m = surv; m; m &= m - 1, ++o) cands.pcell[o] = cbase + (uint32_t)__builtin_ctz(m);
           }
         } else if (k_w) {
           uint32_t o = bn + woff + (uint32_t)ex;
@@ -1233,15 +1290,20 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
             bt[2 * (tn + ti) + 1] = ((bn + woff) << 16) | (uint32_t)k_w;
           }
         }
-        __syncthreads();  // every thread has read cnt[0 .. 5]
-        if (threadIdx.x == 0 && T <= (uint32_t)CAPB) {
-          cnt[4] = bn + T;
-          cnt[5] = tn + nt;
+        __syncthreads();  // every thread has read cnt[0 .. 9]
+        if (threadIdx.x == 0) {
+          if (T <= (uint32_t)CAPB) {
+            cnt[4] = bn + T;
+            cnt[5] = tn + nt;
+          } else {
+            cnt[8] += T;
+            cnt[9] += nt;
+          }
         }
       }
     }  // steps
     __syncthreads();
-    flush();  // the strip's last runs
+    finish(pc0, pt0);  // the strip's runs into the candidate list
   }    // strips
 }
 

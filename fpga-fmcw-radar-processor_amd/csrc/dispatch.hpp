@@ -63,6 +63,7 @@ struct Cfar2Info {
   Cfar2DecideFn decide; // K3b k_cfar2d_decide
   Cfar2EmitFn emit;     // K3c k_cfar2d_emit
   size_t smem;          // K3a's dynamic LDS bytes
+  bool spill;           // K3a writes strip-private spill regions (Cfar2Cands pcell / ptile: k_cfar2d_lv)
 };
 Cfar2Info cfar2_info(uint32_t nc, int hd, int gd, int hr, int gr, bool compat);  // inst_cfar2.hip
 

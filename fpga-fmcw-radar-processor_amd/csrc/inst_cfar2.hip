@@ -20,17 +20,19 @@ template <int N>
 static Cfar2Info info_t(bool lv, int hr, bool compat) {
   Cfar2Fn fn = k_cfar2d<N, 0, 0>;
   size_t smem = cfar2d_smem_bytes<N>(hr);
+  bool spill = false;
   if (lv) {
     if constexpr (rules_kernel<N>()) {
       static_assert(N == 1024, "k_cfar2d_lv stages one 4-cell column per thread (NC = 1024)");
       fn = compat ? k_cfar2d_lv<N, 5, 1, true> : k_cfar2d_lv<N, 5, 1, false>;
       smem = cfar2d_lv_smem_bytes<N, 5, 1>();
+      spill = true;
     } else {
       fn = k_cfar2d<N, 6, 2, 5, 1>;
       smem = cfar2d_smem_bytes<N>(5);
     }
   }
-  return {fn, Cfar2DGeom<N>::TR, k_cfar2d_decide<N>, k_cfar2d_emit<N>, smem};
+  return {fn, Cfar2DGeom<N>::TR, k_cfar2d_decide<N>, k_cfar2d_emit<N>, smem, spill};
 }
 
 Cfar2Info cfar2_info(uint32_t nc, int hd, int gd, int hr, int gr, bool compat) {
@@ -40,7 +42,7 @@ Cfar2Info cfar2_info(uint32_t nc, int hd, int gd, int hr, int gr, bool compat) {
     C_(32) C_(64) C_(128) C_(256) C_(512) C_(1024)
 #undef C_
   }
-  return {nullptr, 0, nullptr, nullptr, 0};
+  return {nullptr, 0, nullptr, nullptr, 0, false};
 }
 
 }  // namespace fmcw

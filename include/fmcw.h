@@ -155,15 +155,15 @@ typedef struct fmcw_config {
   uint32_t range_shift;
   /* fmcw_spectrum_dtype: element type of the internal corner-turned spectrum */
   int32_t spectrum_dtype;
-  /* Detection records the handle's scratch holds for one call beyond each wave tile's own slot
-   * (1/32 of its cells; a denser tile moves its whole run to this shared region).
-   * 0 (default) = every cell of max_frames frames (16 B per cell: 4 GiB at 1024 frames of
-   * 1024 x 256): no call can lose a detection, at any density the CFAR parameters produce -- the
-   * reference emits every non-zero CFAR output (radar_core.vhd:413-418), and cfar_scale_ovr = 1 or
-   * a 1-D alpha of 1 detect ~25 % of noise cells.  N > 0 bounds it to N records, for callers
-   * that bound det_cap: a call then loses records (status word [1]) only when it finds more than
-   * N detections, i.e. never while det_cap <= N would have room for the whole list.
-   * max_frames x cells (+ slots) must stay below 2^32 records. */
+  /* Detection records the handle's scratch holds for one call.  0 (default): a slot of every
+   * cell of each detection tile (16 B per cell of max_frames frames: 4 GiB at 1024 frames of
+   * 1024 x 256), so no call can lose a detection at any density the CFAR parameters produce --
+   * the reference emits every non-zero CFAR output (radar_core.vhd:413-418), and cfar_scale_ovr
+   * = 1 or a 1-D alpha of 1 detect ~25 % of noise cells.  N > 0, for callers that bound det_cap:
+   * slots of 1/32 of a tile's cells plus a shared region of N records for denser tiles; a call
+   * then loses records (status word [1]) only when it finds more than N detections, i.e. never
+   * while det_cap <= N would have room for the whole list.  max_frames x cells must stay below
+   * 2^32 records. */
   uint32_t det_capacity;
 } fmcw_config;
 
@@ -278,7 +278,11 @@ int fmcw_process(fmcw_handle* h, const void* cube, size_t n_frames, float* rd_ma
 
 /* Stage entry points (device pointers, asynchronous).
  * fmcw_cfar reads the map as the RTL's unsigned magnitude stream (magnitude_calc.vhd:45-88):
- * negative cells and -0.0 are taken as +0; NaN / Inf cells are unsupported. */
+ * negative cells and -0.0 are taken as +0.  NaN cells are outside the specification (the RTL's
+ * magnitudes are integers, and the sorting and counting forms of the OS-CFAR disagree on NaN):
+ * a NaN reference never counts, and the 2-D CFAR's level screens (the reference window) take a
+ * NaN CUT as below every level and screen it out, so whether a NaN CUT is reported is not
+ * specified.  +Inf cells are supported. */
 int fmcw_range_ct(fmcw_handle* h, const void* cube, size_t n_frames, void* spec, void* stream);
 int fmcw_magnitude(const float* iq, float* out, size_t n, int mag_mode, void* stream);
 int fmcw_cfar(fmcw_handle* h, const float* map, size_t n_frames, fmcw_det* dets,

@@ -230,3 +230,34 @@ def test_s48_adversarial_dynamic_range(case, spectrum):
     if case == "clutter60":
         got = set(zip(out.dets["frame"].tolist(), out.dets["range"].tolist(), out.dets["doppler"].tolist()))
         assert all((f, 250, 23) in got for f in range(nf))
+
+
+# ---- k_cfar2d_lv on dense / degenerate maps (round 6: strip-private spill, zero-aware strips) ----
+@pytest.mark.parametrize("kind", ["blank_frame", "sparse_denormals", "lognormal_dense"])
+def test_lv_degenerate_maps(kind):
+    """NC = 1024 (k_cfar2d_lv): a frame of zeros beside a Rayleigh frame (a zero-aware strip rules
+    its +0 CUTs out), a 98 % zero map whose non-zero cells include denormals (a denormal CUT is
+    not +0: it is decided exactly), and heavy-tailed clutter whose dense steps go through the
+    strips' private spill regions -- every detection bit-exact vs the C oracle."""
+    ns, nc, nf = 512, 1024, 2
+    rng = np.random.default_rng({"blank_frame": 101, "sparse_denormals": 102, "lognormal_dense": 103}[kind])
+    if kind == "blank_frame":
+        m = rng.rayleigh(1.0, (nf, ns, nc)).astype(np.float32)
+        m[0] = 0.0
+        m[0, 100, 200] = 50.0
+        m[1, 300, 17] = 60.0
+    elif kind == "sparse_denormals":
+        m = np.where(rng.random((nf, ns, nc)) < 0.02, rng.rayleigh(10.0, (nf, ns, nc)), 0.0).astype(np.float32)
+        tiny = rng.random((nf, ns, nc)) < 0.002
+        m[tiny] = np.float32(1e-40)                    # denormal cells among the zeros
+        m[0, 60, 100] = 4000.0
+    else:
+        m = rng.lognormal(1.0, 1.2, (nf, ns, nc)).astype(np.float32)
+    want = CB.cfar(m, O.Cfar2D(), threads=16, cap=1 << 22)
+    assert len(want) > 0
+    with RadarCore(N_RANGE=ns, N_DOPPLER=nc, cfar="os2d", max_frames=nf) as core:
+        st, got = _run_cfar(core, m, m.size)
+    assert int(st[0]) == len(want) and st[1] == 0
+    np.testing.assert_array_equal(got, want)
+    if kind == "sparse_denormals":
+        assert (got["mag"] < 1e-30).any()              # some denormal CUTs do detect

@@ -4,7 +4,9 @@ cells that survive the s_min rule and the scale rules A / B, per pair of level q
 QB clamped to 1.5 QA as the kernel does), with the kernel's bounds for levels C (16 cells around a
 group of 4 CUTs) and D (the lane's 11 x 32 window).  The map is the bench's synthetic config-5 frame
 (seed 1234) through the C restatement (oracle/fmcw_cpu.c); 4 x 48 CUT rows.
-usage: python tools/k3_rules_model.py [--pairs 0.56:0.68,0.50:0.74]"""
+usage: python tools/k3_rules_model.py [--pairs 0.56:0.68,0.50:0.74] [--law bench|rayleigh|exponential|lognormal|uniform]
+(--law: synthetic clutter instead of the bench frame, as tools/cfar2d_bench.py --maps; the share of
+survivors that truly detect is printed beside them)"""
 import argparse
 import sys
 from pathlib import Path
@@ -28,15 +30,28 @@ def lo(k):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pairs", default="0.56:0.68,0.52:0.68,0.56:0.74,0.50:0.74,0.48:0.76")
+    ap.add_argument("--law", default="bench")
     a = ap.parse_args()
     pairs = [tuple(float(x) for x in p.split(":")) for p in a.pairs.split(",")]
     import cpu_backend as CB
+    import fmcw_oracle as O
     from fmcw import synth
-    cube = synth.frames(1, 8192, 1024, 1, "two_targets", seed=1234, dtype="f16")
-    if not np.iscomplexobj(cube):
-        x = cube.astype(np.float32)
-        cube = x[..., 0] + 1j * x[..., 1]
-    m = CB.process(cube.astype(np.complex64), None, threads=8)[0][0]
+    if a.law == "bench":
+        cube = synth.frames(1, 8192, 1024, 1, "two_targets", seed=1234, dtype="f16")
+        if not np.iscomplexobj(cube):
+            x = cube.astype(np.float32)
+            cube = x[..., 0] + 1j * x[..., 1]
+        m = CB.process(cube.astype(np.complex64), None, threads=8)[0][0]
+    else:
+        rng = np.random.default_rng(7)
+        sh = (8192, 1024)
+        m = {"rayleigh": lambda: rng.rayleigh(1.0, sh), "exponential": lambda: rng.exponential(5.0, sh),
+             "lognormal": lambda: rng.lognormal(1.0, 1.2, sh), "uniform": lambda: rng.uniform(9.0, 11.0, sh)}[a.law]()
+        m = m.astype(np.float32)
+    dets = {}
+    for r0 in [20, 2055, 4096, 6124]:
+        d, _ = O.cfar_os2d(m[r0 - HR:r0 + NROWS + HR], O.Cfar2D())
+        dets[r0] = d[HR:-HR]
     s_min, s2 = np.float32(2.0), np.float32(4.0)
     tot = {p: [] for p in pairs}
     for r0 in [20, 2055, 4096, 6124]:
@@ -77,8 +92,12 @@ def main():
             smin = ((CA >= NEED) & (cut < UA)) | ((CB_ >= NEED) & (cut < UB))
             rB = (CB_ >= NEED) & (CB_ <= 63) & (CC <= 32) & ~nzD & (cut < U2B)
             rA = rule_a & (CA >= NEED) & (CA <= 80) & (CB_ <= 40) & (CC <= 8) & ~nzD & (cut < U2A)
-            tot[p].append((~(smin | rA | rB)).mean())
-    print({f"{p[0]:.2f}/{p[1]:.2f}": "%.4f %%" % (100 * np.mean(v)) for p, v in tot.items()})
+            surv = ~(smin | rA | rB)
+            assert not (dets[r0] & ~surv).any(), "the screen dropped a detection"
+            tot[p].append((surv.mean(), dets[r0].mean()))
+    print(a.law, {f"{p[0]:.2f}/{p[1]:.2f}": "survivors %.4f %% (detect %.4f %%)" % (100 * np.mean([x[0] for x in v]),
+                                                                         100 * np.mean([x[1] for x in v]))
+                  for p, v in tot.items()})
 
 
 if __name__ == "__main__":
