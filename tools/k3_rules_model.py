@@ -31,6 +31,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pairs", default="0.56:0.68,0.52:0.68,0.56:0.74,0.50:0.74,0.48:0.76")
     ap.add_argument("--law", default="bench")
+    ap.add_argument("--kd", type=int, default=2, help="level D = QB + kd octaves (the kernel: 2)")
+    ap.add_argument("--rb", default="63:32", help="rule B bounds C_B:C_C")
+    ap.add_argument("--ra", default="80:40:8", help="rule A bounds C_A:C_B:C_C")
     a = ap.parse_args()
     pairs = [tuple(float(x) for x in p.split(":")) for p in a.pairs.split(",")]
     import cpu_backend as CB
@@ -83,15 +86,17 @@ def main():
         for p in pairs:
             QA = int(np.quantile(k7, p[0])) * 8
             QB = max(QA, min(int(np.quantile(k7, p[1])) * 8, int(k16(np.float32(1.5) * lo(QA)))))
-            QC, QD = QB + 128, QB + 256
+            QC, QD = QB + 128, QB + 128 * a.kd
             CA, CB_ = box(QA), box(QB)
             CC, nzD = window(QC, 4, -6, 10), window(QD, 16, -8, 24) > 0
             UA, UB = int(k16(s_min * lo(QA))), int(k16(s_min * lo(QB)))
             U2A, U2B = int(k16(s2 * lo(QA))), int(k16(s2 * lo(QB)))
             rule_a = lo(QB) <= 1.5 * lo(QA)
             smin = ((CA >= NEED) & (cut < UA)) | ((CB_ >= NEED) & (cut < UB))
-            rB = (CB_ >= NEED) & (CB_ <= 63) & (CC <= 32) & ~nzD & (cut < U2B)
-            rA = rule_a & (CA >= NEED) & (CA <= 80) & (CB_ <= 40) & (CC <= 8) & ~nzD & (cut < U2A)
+            b1, b2 = (int(x) for x in a.rb.split(":"))
+            a1, a2, a3 = (int(x) for x in a.ra.split(":"))
+            rB = (CB_ >= NEED) & (CB_ <= b1) & (CC <= b2) & ~nzD & (cut < U2B)
+            rA = rule_a & (CA >= NEED) & (CA <= a1) & (CB_ <= a2) & (CC <= a3) & ~nzD & (cut < U2A)
             surv = ~(smin | rA | rB)
             assert not (dets[r0] & ~surv).any(), "the screen dropped a detection"
             tot[p].append((surv.mean(), dets[r0].mean()))
