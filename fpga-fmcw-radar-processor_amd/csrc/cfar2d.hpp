@@ -741,8 +741,15 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
             int trow, d;
             const uint32_t e = list[j];
             cell_of(e, trow, d);
-            if (cfar2d_exact_a<NC, HD, GD>(rr, trow, key_hi(rr.krow(trow + a.hr)[k16idx(d)]), d, a, need, sub, L) &&
-                sub == 0)
+            const uint32_t kc = rr.krow(trow + a.hr)[k16idx(d)];
+            // a +0 CUT never detects (every reference is >= it: E(s) = n_ref), but with key16 0 it passes
+            // every key bound; the exact cell decides (only key-0 cells load it: blank / sparse maps)
+            bool live = true;
+            if (kc == 0u) {
+              const float v = fm[(size_t)(r0 + trow) * NC + d];
+              live = (a.compat ? q17(v) : nonneg(v)) > 0.f;
+            }
+            if (live && cfar2d_exact_a<NC, HD, GD>(rr, trow, key_hi(kc), d, a, need, sub, L) && sub == 0)
             {
               atomicOr(&aux[e >> 4], 1u << (e & 15u));
               atomicAdd(&cnt[13], 1u);
@@ -758,29 +765,51 @@ k_cfar2d(const float* __restrict__ map, int ns, int n_strips, int steps, int fra
       // candidate list as one contiguous run (k_cfar2d_decide decides them, k_cfar2d_emit writes
       // the tile's records); (wg_base, wg_count) = (run start, run length) until then.  An empty
       // tile is final here.
-      if (has_tile) {
-        uint32_t mine = 0u;
-        if (n_cand != 0u) mine = cand;  // bits of this lane's candidates (cand: aux after the test)
+      // One reservation (two atomics) per workgroup step with candidates, not per wave tile (round 6:
+      // on heavy-tailed clutter, where most wave tiles have candidates, the per-tile atomics on the
+      // launch's two counters serialised; n_cand != 0 is uniform over the workgroup).
+      if (n_cand != 0u) {
+        const uint32_t mine = has_tile ? cand : 0u;  // bits of this lane's candidates (aux after the test)
         int k_w;
         const int ex = wave_excl_scan(__popc(mine), k_w);
-        if (k_w == 0) {
-          if (lane == 0) {
-            sink.wg_base[wtile] = (uint32_t)wtile * sink.slot_cap;
-            sink.wg_count[wtile] = 0u;
-          }
-        } else {
-          uint32_t p0 = 0u;
-          if (lane == 0) {
-            p0 = atomicAdd(&cands.ctr[0], (uint32_t)k_w);
-            cands.tiles[atomicAdd(&cands.ctr[1], 1u)] = (uint32_t)wtile;
-            sink.wg_base[wtile] = p0;
-            sink.wg_count[wtile] = (uint32_t)k_w;
-          }
-          p0 = (uint32_t)__shfl((int)p0, 0, 64);
-          const uint32_t cbase = ((uint32_t)f * (uint32_t)ns + (uint32_t)r) * (uint32_t)NC + (uint32_t)d0;
-          uint32_t o = p0 + (uint32_t)ex;
-          for (uint32_t m = mine; m; m &= m - 1, ++o) cands.cell[o] = cbase + (uint32_t)__builtin_ctz(m);
+        if (lane == 0) cnt[8 + wv] = has_tile ? (uint32_t)k_w : 0u;
+        __syncthreads();
+        uint32_t T = 0, woff = 0, ti = 0, nt = 0;
+#pragma unroll
+        for (int i = 0; i < WPB; ++i) {
+          const uint32_t c = cnt[8 + i];
+          woff += i < wv ? c : 0u;
+          ti += (i < wv && c) ? 1u : 0u;
+          T += c;
+          nt += c ? 1u : 0u;
         }
+        if (threadIdx.x == 0) {
+          cnt[6] = atomicAdd(&cands.ctr[0], T);
+          cnt[7] = atomicAdd(&cands.ctr[1], nt);
+        }
+        __syncthreads();
+        const uint32_t p0 = cnt[6] + woff, q0 = cnt[7] + ti;
+        if (has_tile) {
+          if (k_w == 0) {
+            if (lane == 0) {
+              sink.wg_base[wtile] = (uint32_t)wtile * sink.slot_cap;
+              sink.wg_count[wtile] = 0u;
+            }
+          } else {
+            if (lane == 0) {
+              cands.tiles[q0] = (uint32_t)wtile;
+              sink.wg_base[wtile] = p0;
+              sink.wg_count[wtile] = (uint32_t)k_w;
+            }
+            const uint32_t cbase = ((uint32_t)f * (uint32_t)ns + (uint32_t)r) * (uint32_t)NC + (uint32_t)d0;
+            uint32_t o = p0 + (uint32_t)ex;
+            for (uint32_t m = mine; m; m &= m - 1, ++o) cands.cell[o] = cbase + (uint32_t)__builtin_ctz(m);
+          }
+        }
+        __syncthreads();  // cnt[6 .. 11] are read before the next step rewrites them
+      } else if (has_tile && lane == 0) {
+        sink.wg_base[wtile] = (uint32_t)wtile * sink.slot_cap;
+        sink.wg_count[wtile] = 0u;
       }
     }  // steps
   }    // strips
