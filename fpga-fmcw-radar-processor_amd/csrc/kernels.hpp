@@ -1716,6 +1716,8 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
       pass_sync<false>();
       {
         // one prefetch site: two (one per branch) merged their register results through copies
+        // (round 6: issued right after the strided-S48 decode instead, config 2 K2 measured 64.5-67.8
+        // against 64.7-65.3 us per launch, profiles/r06/k2_early_pf/)
         const bool same = rx + 1 < nrx;
         prefetch(same ? tile : tile + tile_step, same ? rx + 1 : 0);
       }
