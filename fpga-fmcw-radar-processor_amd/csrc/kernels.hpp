@@ -1439,10 +1439,8 @@ __device__ __forceinline__ int xcd_block_id(int bid, int grid) {
 // SIMD (config-3 K2 41.6-41.9 -> 39.0-39.2 us per launch, profiles/r03/k2/k2_pf_ab.log; 16 points
 // 42.1, none 42.2-42.5); none at NC = 1024 (8 or 16 points: 61-64 against 56 us).
 template <int NC, int MTI>
-#ifndef FMCW_LAB_PF512
-#define FMCW_LAB_PF512 8
-#endif
-constexpr int k2_prefetch() { return MTI != 0 ? 0 : NC <= 256 ? 16 : NC == 512 ? FMCW_LAB_PF512 : 0; }
+// (Round 6, config 3: 4 points ahead 38.4-38.9 against 35.8-35.9 us per launch, profiles/r06/k2_c3_ab/.)
+constexpr int k2_prefetch() { return MTI != 0 ? 0 : NC <= 256 ? 16 : NC == 512 ? 8 : 0; }
 // FAST (below) at NC = 256 fits 128 VGPRs without scratch: 4 waves per SIMD (4 workgroups of
 // 39 KiB LDS per CU); measured K2 58.2 -> 56.0 us per 96-frame launch at config 2.  At NC = 512
 // / 1024 the fourth wave costs more than it hides (config 3 K2 41.7 -> 55.9 us, config 5 55.5
@@ -1621,10 +1619,8 @@ k_doppler(const float2* __restrict__ inter_in, const float* __restrict__ win_d, 
   // (measured: config 5 K2 177 -> 110 us per 4 frames; configs 2 / 3, whose workgroups read
   // whole lines, 2-3 % slower with it)
   // (S48: its 6-B points, so config 3's 96-B reads take the XCD mapping too)
-#ifndef FMCW_LAB_XCD512
-#define FMCW_LAB_XCD512 0
-#endif
-  const bool xcd = ((WPB * WR * (S48F || S48S ? 6 : 8)) << lgT) < 128 || (FMCW_LAB_XCD512 && NC == 512);
+  // (round 6, config 3 with the remap: K2 37.0-37.9 against 35.8-35.9 us per launch, profiles/r06/k2_c3_ab/)
+  const bool xcd = ((WPB * WR * (S48F || S48S ? 6 : 8)) << lgT) < 128;
   const int bid = xcd ? xcd_block_id((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
   prefetch(bid * WPB + wv, 0);
 
