@@ -44,7 +44,7 @@ sys.path.insert(0, str(REPO / "fpga-fmcw-radar-processor_amd"))
 
 HBM_PEAK_GBPS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CLOCK_GHZ = 2.4             # MI355X peak engine clock
-PMC_FILE = "pmc_r05.json"   # per-frame HBM bytes and SQ counts per workload (tools/pmc_summary.py)
+PMC_FILE = "pmc_r06.json"   # per-frame HBM bytes and SQ counts per workload (tools/pmc_summary.py)
 
 WORKLOADS = {
     "c2": dict(ns=1024, nc=256, nrx=1, dtype="f32", cfar="os1d", frames=1024, recipe="two_targets", spectrum="s48",
