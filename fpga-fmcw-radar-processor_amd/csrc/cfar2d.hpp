@@ -891,7 +891,7 @@ __device__ __forceinline__ uint32_t lv_cut_code(uint2 kw, const uint32_t (&W)[4]
 template <int HR, int GR>
 __device__ __forceinline__ uint32_t cfar2d_screen_prefix(const uint8_t* hiA, const uint8_t* loA, const uint8_t* hiC,
                                                          const uint8_t* loC, const uint8_t* hiG, const uint8_t* loG,
-                                                         uint2 cw, int need, bool ruleA, bool zaware) {
+                                                         uint2 cw, int need, bool ruleA) {
   static_assert((2 * HR + 1) * 13 - (2 * GR + 1) * 5 == 128 && 2 * HR + 1 <= 15 && 5 * (2 * GR + 1) <= 15,
                 "thresholds below are for n_ref 128");
   uint32_t V[8], G[6], W[8];
@@ -978,10 +978,6 @@ __device__ __forceinline__ uint32_t cfar2d_screen_prefix(const uint8_t* hiA, con
     const uint32_t rB = nb2 & ~(CB + K(64)) & okC32[m] & okD & (nb << 4);   // C_B <= 63, C_C <= 32
     const uint32_t rA = na & ~(CA + K(47)) & ~(CB + K(87)) & okC8[m] & okA & (nb << 5);  // 80, 40, 8
     sv[m] = ~(smin | rA | rB) & H;
-    if (zaware) {  // uniform: code 0x1 (no key16 gives it) marks a +0 CUT, which never detects
-      const uint32_t x = nb ^ 0x01010101u;        // bytes <= 0x0F: + 0x7F sets bit 7 iff the byte is not 0
-      sv[m] &= (x + 0x7F7F7F7Fu);
-    }
   }
   // the survivor bits in cell order, only where there are any (a few lanes in a thousand)
   uint32_t bits = 0;
@@ -1090,11 +1086,14 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
   uint32_t qa2 = 0, qb2 = 0, qc2 = 0, qd2 = 0;
   uint32_t Wc[4] = {0, 0, 0, 0};
   bool ruleA = false;
-  // zero-aware strip (most of its first step's cells are +0 or tiny: a sparse or blank map): the cut
-  // code of a +0 CUT becomes 0x1, which the screen rules out -- E(s) counts every reference of a +0
-  // CUT (refs >= +0), so it cannot detect.  Without it every +0 cell of such a strip survived the
-  // level rules (its refs are mostly below every level) and K3b decided all of them: 26.8 ms per
-  // 16-frame launch on a map with 98 % zeros (round 6, tools/cfar2d_bench.py --maps sparse).
+  // zero-aware strip (most of its first step's cells are +0 or tiny: a sparse or blank map): the
+  // screen's survivors lose their +0 CUTs -- E(s) counts every reference of a +0 CUT (refs >= +0), so
+  // it cannot detect.  Without it every +0 cell of such a strip survived the level rules (its refs
+  // are mostly below every level) and K3b decided all of them: 26.8 ms per 16-frame launch on a map
+  // with 98 % zeros (round 6, tools/cfar2d_bench.py --maps sparse).  The filter re-reads the
+  // survivors' cells from the map (L2, just staged) behind a uniform branch, so the staging and the
+  // screen carry no zero-aware work (as a cut code 0x1 set in staging and ruled out by the screen:
+  // 228 against 226 us per config-5 launch on the bench map, profiles/r06/k3_zaware/).
   bool zaware = false;
   uint32_t pab = 0, pcd = 0;  // this column's running prefixes (A / B, C / D)
   // one ring slot's cells dt .. dt + 3: level bits into the prefixes, prefixes and cut codes to LDS
@@ -1121,12 +1120,7 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
       *reinterpret_cast<uint32_t*>(rp + pidx(dt - NC)) = pab;
       *reinterpret_cast<uint32_t*>(rp + RB + pidx(dt - NC)) = pcd;
     }
-    uint32_t code = lv_cut_code(kw, Wc);
-    if (zaware) {  // uniform: +0 cells (s == 0 after the sanitising) get code 0x1
-      const uint32_t z = (s0 == 0u ? 0x000Fu : 0u) | (s1 == 0u ? 0x00F0u : 0u) | (s2 == 0u ? 0x0F00u : 0u) |
-                         (s3 == 0u ? 0xF000u : 0u);
-      code = (code & ~z) | (z & 0x1111u);
-    }
+    const uint32_t code = lv_cut_code(kw, Wc);
     *reinterpret_cast<uint16_t*>(rp + 2 * RB + dt / 2) = (uint16_t)code;
   };
 
@@ -1274,7 +1268,22 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
         const uint8_t* const lA = up ? p_hi : p_lo;
         const uint8_t* const hG = up ? g_lo : g_hi;
         const uint8_t* const lG = up ? g_hi : g_lo;
-        surv = cfar2d_screen_prefix<HR, GR>(hA, lA, hA + RB, lA + RB, hG, lG, cw, need, ruleA, zaware);
+        surv = cfar2d_screen_prefix<HR, GR>(hA, lA, hA + RB, lA + RB, hG, lG, cw, need, ruleA);
+        if (zaware && surv) {  // uniform flag: drop the +0 CUTs, re-read from the map (L2: just staged)
+          uint32_t z = 0;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            float4 q = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)((r * NC + d0 + 4 * u) * 4), 0, 0));
+            if constexpr (CMP) q = q17x4(q);
+            const float e[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const uint32_t b = __float_as_uint(e[j]);  // s == 0 after staging's sanitising
+              z |= (b == 0u || b > 0x7f800000u ? 1u : 0u) << (4 * u + j);
+            }
+          }
+          surv &= ~z;
+        }
       }
       // emission: each wave tile's survivors, in (range, doppler) order, as one run of the strip
       // buffer (flushed to the candidate list when full and at the strip's end); an empty tile is
