@@ -41,6 +41,13 @@ KERNEL(k_lshl_add64, uint64_t, threadIdx.x + i, asm volatile("v_lshl_add_u64 %0,
 KERNEL(k_lshr64, uint64_t, threadIdx.x + i, asm volatile("v_lshrrev_b64 %0, 1, %0" : "+v"(a[i])))
 KERNEL(k_sqrt, float, threadIdx.x * 0.001f + i + 1.f, asm volatile("v_sqrt_f32 %0, %0" : "+v"(a[i])))
 KERNEL(k_cndmask, uint32_t, threadIdx.x + i, asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(s) : "vcc"))
+// (round 6) integer multiply and the cndmask forms the K3 screen compiles to; the mask set once
+// outside the chains (the row above declares vcc clobbered, so every instance waits on a VALU write)
+KERNEL(k_mul_lo, uint32_t, threadIdx.x + i, asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[i]) : "v"(s)))
+KERNEL(k_mul_u24, uint32_t, threadIdx.x + i, asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(a[i]) : "v"(s)))
+KERNEL(k_lshl_add, uint32_t, threadIdx.x + i, asm volatile("v_lshl_add_u32 %0, %0, 8, %0" : "+v"(a[i])))
+KERNEL(k_cnd_sgpr, uint32_t, threadIdx.x + i, asm volatile("v_cndmask_b32_e64 %0, 0, %0, %1" : "+v"(a[i]) : "s"((uint64_t)s * 0x5555u)))
+KERNEL(k_cmp_cnd, uint32_t, threadIdx.x + i, asm volatile("v_cmp_gt_u32_e64 s[40:41], 33, %0\n\tv_cndmask_b32_e64 %0, 0, %0, s[40:41]" : "+v"(a[i]) :: "s40", "s41"))
 
 struct K { const char* name; void* fn; };
 int main() {
@@ -57,7 +64,9 @@ int main() {
             {"v_bitop3_b32", (void*)k_bitop3}, {"v_fma_f32", (void*)k_fma}, {"v_add_f32", (void*)k_add_f32},
             {"v_pk_add_f32", (void*)k_pk_add}, {"v_pk_fma_f32", (void*)k_pk_fma}, {"v_pk_mul_f32", (void*)k_pk_mul},
             {"v_fmac_f32", (void*)k_fmac}, {"v_mul_f32", (void*)k_mul_f32}, {"v_sub_f32", (void*)k_sub_f32}, {"v_lshl_add_u64", (void*)k_lshl_add64},
-            {"v_lshrrev_b64", (void*)k_lshr64}, {"v_sqrt_f32", (void*)k_sqrt}, {"v_cndmask_b32", (void*)k_cndmask}};
+            {"v_lshrrev_b64", (void*)k_lshr64}, {"v_sqrt_f32", (void*)k_sqrt}, {"v_cndmask_b32", (void*)k_cndmask},
+            {"v_mul_lo_u32", (void*)k_mul_lo}, {"v_mul_u32_u24", (void*)k_mul_u24}, {"v_lshl_add_u32", (void*)k_lshl_add},
+            {"v_cndmask sgpr", (void*)k_cnd_sgpr}, {"v_cmp+v_cndmask", (void*)k_cmp_cnd}};
   const int grid = n_cu * 4;  // 256 threads = one wave per SIMD per workgroup -> 4 waves per SIMD
   const double instr = (double)grid * 4 * ITER * CH;
   for (const K& k : ks) {
