@@ -883,6 +883,20 @@ __device__ __forceinline__ uint32_t lv_cut_code(uint2 kw, const uint32_t (&W)[4]
   const uint32_t t = n | (n >> 4);        // byte 0 = cells 0, 1; byte 2 = cells 2, 3
   return (t & 0xffu) | ((t >> 8) & 0xff00u);
 }
+// The same when U_1 = QC and U_3 = QD (the default scales, s_min = 2 and s2 = 4: fl(2 lo(QB)) and
+// fl(4 lo(QB)) are lo(QB + 128) and lo(QB + 256)): flags 1 and 3 are then the complements of the
+// cells' own C / D level bits, which staging has already formed (wcd: byte j bit 0 = key16 >= QC,
+// bit 4 = key16 >= QD), so only flags 0 and 2 take compares.
+__device__ __forceinline__ uint32_t lv_cut_code_cd(uint2 kw, const uint32_t (&W)[4], uint32_t wcd) {
+  uint32_t n = (((wcd << 1) & 0x02020202u) | ((wcd >> 1) & 0x08080808u)) ^ 0x0a0a0a0au;
+#pragma unroll
+  for (int k = 0; k < 4; k += 2) {
+    const uint32_t f = __builtin_amdgcn_perm(W[k] - kw.y, W[k] - kw.x, 0x07050301u);
+    n |= (f >> (7 - k)) & (0x01010101u << k);
+  }
+  const uint32_t t = n | (n >> 4);
+  return (t & 0xffu) | ((t >> 8) & 0xff00u);
+}
 
 // Survivor bits (bit j: cell d0 + j may detect) of a lane's 16 CUTs from the prefix rows: hiA / loA
 // (A / B levels) and hiC / loC (C / D) the 32-byte windows (cells d0 - 8 .. d0 + 23) of the two rows
@@ -1086,6 +1100,7 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
   uint32_t qa2 = 0, qb2 = 0, qc2 = 0, qd2 = 0;
   uint32_t Wc[4] = {0, 0, 0, 0};
   bool ruleA = false;
+  bool cd_codes = false;  // U_B == QC and U2_B == QD: lv_cut_code_cd
   // zero-aware strip (most of its first step's cells are +0 or tiny: a sparse or blank map): the
   // screen's survivors lose their +0 CUTs -- E(s) counts every reference of a +0 CUT (refs >= +0), so
   // it cannot detect.  Without it every +0 cell of such a strip survived the level rules (its refs
@@ -1107,8 +1122,9 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
     const uint32_t s0 = b0 <= 0x7f800000u ? b0 : 0u, s1 = b1 <= 0x7f800000u ? b1 : 0u;
     const uint32_t s2 = b2 <= 0x7f800000u ? b2 : 0u, s3 = b3 <= 0x7f800000u ? b3 : 0u;
     const uint2 kw = make_uint2(__builtin_amdgcn_perm(s1, s0, 0x07060302u), __builtin_amdgcn_perm(s3, s2, 0x07060302u));
+    const uint32_t wcd = lv_nibbles_add(kw, qc2, qd2);
     pab = nib_add(pab, lv_nibbles_add(kw, qa2, qb2));
-    pcd = nib_add(pcd, lv_nibbles_add(kw, qc2, qd2));
+    pcd = nib_add(pcd, wcd);
     uint8_t* const rp = ring + slot * ROWB;
     *reinterpret_cast<uint32_t*>(rp + pidx(dt)) = pab;
     *reinterpret_cast<uint32_t*>(rp + RB + pidx(dt)) = pcd;
@@ -1120,7 +1136,7 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
       *reinterpret_cast<uint32_t*>(rp + pidx(dt - NC)) = pab;
       *reinterpret_cast<uint32_t*>(rp + RB + pidx(dt - NC)) = pcd;
     }
-    const uint32_t code = lv_cut_code(kw, Wc);
+    const uint32_t code = cd_codes ? lv_cut_code_cd(kw, Wc, wcd) : lv_cut_code(kw, Wc);  // (uniform)
     *reinterpret_cast<uint16_t*>(rp + 2 * RB + dt / 2) = (uint16_t)code;
   };
 
@@ -1215,6 +1231,8 @@ k_cfar2d_lv(const float* __restrict__ map, int ns, int n_strips, int steps, int 
         const uint32_t UA = key16(a.s_min * key_lo(QA)), UB = key16(a.s_min * key_lo(QB));
         const uint32_t U2A = s2ok ? key16(s2 * key_lo(QA)) : 0u, U2B = s2ok ? key16(s2 * key_lo(QB)) : 0u;
         ruleA = s2ok && key_lo(QB) <= 1.5f * key_lo(QA);
+        // equal thresholds make "key16 < U" and "not key16 >= Q" the same predicate, whatever the scales
+        cd_codes = UB == QC && U2B == QD;
         zaware = QA < 16u;  // the 50 % quantile level below 2^-124: at least half the cells are ~zero
         const uint32_t U[4] = {UA, UB, U2A, U2B};
 #pragma unroll
