@@ -1,3 +1,9 @@
+#!/usr/bin/env bash
+# Round 6: K3 A/B on the GPU box -- the 2-D CFAR GPU tests with the in-tree library, then
+# tools/cfar2d_bench.py (configs 3 / 5, bench maps) interleaved: libfmcw.so ("new") against
+# lib/var_base.so ("base", the library before the change, built on the CPU host with
+# `git stash; tools/build_variants.sh base=-DFMCW_VAR_BASE=1; git stash pop`).
+# usage (gpurun): bash tools/k3_cd_ab.sh    logs: gpurun_out/r06d/
 set -u
 O=gpurun_out/r06d; mkdir -p $O
 export TMPDIR=/tmp
